@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPU counter samples/sec + tracing overhead on a
+Llama-3-8B DDP training step (BASELINE.json metric / config).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (driver does this for N>1)
+
+Per rank: the in-process agent samples 14 SQ/TCC/GRBM counters of its
+MI355X through rocprofiler-sdk device counting at --sample-hz, packs them
+with the CDNA4 sampler_pack kernel into an HBM ring, and every training step
+gathers the new slots to rank 0 over RCCL (ncclGather, xGMI).  Rank 0 drains
+them over PCIe, aggregates per GPU and logs through the Logger sinks.
+
+Timed phases (each bracketed by barrier + cuda.synchronize, max over ranks):
+  1. baseline: K steps with the agent paused (no sampling, no gathers)
+  2. measured: K steps with sampling + per-step gather   -> ms_per_step
+value = counter samples (taken inside phase 2's window and delivered to
+rank 0) / window seconds, summed over all GPUs.  overhead % = phase2/phase1-1.
+Data: synthetic random tokens; weights: random init of the full Llama-3-8B.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+METRIC = "counter samples/sec/GPU + tracing overhead % on Llama-3-8B train, 1/2/4/8 MI355X"
+# Reference effective GPU counter rate: DCGM watch every 10 s = 0.1 samples/s/GPU
+# (BASELINE.md row "GPU metric sampling interval (DCGM)", dynolog/src/Main.cpp:42-45).
+BASELINE_SAMPLES_PER_SEC_PER_GPU = 0.1
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--model", default="llama3-8b")
+    p.add_argument("--micro-batch", type=int, default=2)
+    p.add_argument("--seq-len", type=int, default=4096)
+    p.add_argument("--sample-hz", type=float, default=1000.0)
+    p.add_argument("--pack-batch", type=int, default=32)
+    p.add_argument("--gather-mode", default="gather", choices=["gather", "allgather", "none"])
+    p.add_argument("--no-agent", action="store_true", help="run the workload only")
+    p.add_argument("--skip-baseline", action="store_true")
+    p.add_argument("--log-file", default="", help="agent log destination (default stderr)")
+    p.add_argument("--json-out", default="", help="also write the result line here")
+    return p.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world_env == 1:
+        # Convenience: re-launch ourselves under torchrun (before any GPU init).
+        import subprocess
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+               "--master-port=29533", os.path.abspath(__file__)] + (argv or sys.argv[1:])
+        return subprocess.call(cmd)
+
+    use_agent = not args.no_agent
+    if use_agent:
+        from dynolog_amd import agent as dagent
+        dagent.preinit()  # rocprofiler-sdk tool registration: before HIP init
+
+    import torch
+    from dynolog_amd.models.llama import CONFIGS, build_llama, lm_loss
+    from dynolog_amd.parallel import dist as pdist
+
+    env = pdist.init()
+    dev = torch.device("cuda", env.local_rank)
+    torch.manual_seed(1234 + env.rank)
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+    cfg = CONFIGS[args.model]
+    model = build_llama(args.model, device=dev, dtype=torch.bfloat16, seed=0)
+    model = pdist.wrap_ddp(model, env)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-5, betas=(0.9, 0.95),
+                            weight_decay=0.1, fused=True)
+    B, S = args.micro_batch, args.seq_len
+    data = torch.randint(0, cfg.vocab_size, (B, S + 1), device=dev)
+    inputs, targets = data[:, :-1].contiguous(), data[:, 1:].contiguous()
+
+    ag = None
+    if use_agent:
+        ag = dagent.GpuAgent.start(device=env.local_rank, rank=env.rank, world=env.world,
+                                   sample_hz=args.sample_hz, batch=args.pack_batch,
+                                   gather_mode=args.gather_mode, log_file=args.log_file,
+                                   sinks=("json", "memory"))
+
+    last_loss = [0.0]
+
+    def train_step():
+        logits = model(inputs)
+        loss = lm_loss(logits, targets)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        if ag is not None:
+            ag.step()  # rank-0 gather of new counter slots, on the current stream
+        last_loss[0] = loss
+
+    def timed(k: int) -> tuple[float, int, int]:
+        pdist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m0 = dagent.mono_ns() if ag else 0
+        for _ in range(k):
+            train_step()
+        torch.cuda.synchronize()
+        pdist.barrier()
+        t1 = time.perf_counter()
+        m1 = dagent.mono_ns() if ag else 0
+        return pdist.all_reduce_max(t1 - t0), m0, m1
+
+    for _ in range(args.warmup):
+        train_step()
+    torch.cuda.synchronize()
+
+    base_s = None
+    if ag is not None and not args.skip_baseline:
+        ag.pause()
+        time.sleep(0.05)
+        base_s, _, _ = timed(args.steps)
+        ag.resume()
+        for _ in range(2):  # let sampling re-settle outside the window
+            train_step()
+        torch.cuda.synchronize()
+
+    meas_s, m0, m1 = timed(args.steps)
+    loss_val = float(last_loss[0].item()) if torch.is_tensor(last_loss[0]) else last_loss[0]
+
+    total_samples = 0
+    per_rank = []
+    agent_stats = {}
+    if ag is not None:
+        # deliver every sample taken inside the window (untimed catch-up gather)
+        ag.pack_pending()
+        pdist.barrier()
+        ag.step()
+        torch.cuda.synchronize()
+        pdist.barrier()
+        if env.rank == 0:
+            ag.flush()
+            per_rank = ag.window_counts(m0, m1)
+            total_samples = sum(per_rank)
+            agent_stats = ag.stats()
+
+    window_s = (m1 - m0) * 1e-9 if ag is not None else meas_s
+    value = total_samples / window_s if window_s > 0 else 0.0
+    tokens = B * S * env.world * args.steps
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "counter_samples/s",
+        "n_gpus": env.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(meas_s / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (BASELINE_SAMPLES_PER_SEC_PER_GPU * env.world), 2),
+        "dtype": "bf16",
+        "data": "synthetic (random tokens; random-init Llama-3-8B weights)",
+        "config": {
+            "model": args.model, "global_batch": B * env.world, "seq_len": S,
+            "parallelism": f"dp{env.world}", "sample_hz_target": args.sample_hz,
+            "counters": 14, "gather": args.gather_mode, "pack_batch": args.pack_batch,
+        },
+        "samples_per_sec_per_gpu": round(value / env.world, 3),
+        "samples_per_rank": per_rank,
+        "baseline_ms_per_step": round(base_s / args.steps * 1e3, 3) if base_s else None,
+        "tracing_overhead_pct": round((meas_s / base_s - 1.0) * 100.0, 3) if base_s else None,
+        "tokens_per_sec": round(tokens / meas_s, 1),
+        "loss": round(loss_val, 4),
+        "vs_baseline_note": "value / (0.1 samples/s/GPU x n_gpus): reference DCGM 10 s interval",
+    }
+    if agent_stats:
+        out["agent"] = {k: agent_stats.get(k) for k in
+                        ("samples_taken", "samples_failed", "sample_latency_us_avg",
+                         "sample_latency_us_max", "late_ticks", "gathers", "raw_instances",
+                         "last_error")}
+    if env.rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if ag is not None:
+        ag.stop()
+    pdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

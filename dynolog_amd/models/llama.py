@@ -1,0 +1,165 @@
+"""Llama-3 family decoder (random init) used as the synthetic training
+workload for tracing-overhead and counter-rate measurements.
+
+The reference ships only a toy linear model as its tracing target
+(scripts/pytorch/linear_model_example.py:1-86); BASELINE.json names a
+Llama-3-8B training step as the workload, so that is the flagship config.
+Architecture (Llama-3-8B): d_model 4096, 32 layers, 32 query heads, 8 KV heads
+(GQA), head_dim 128, SwiGLU FFN 14336, vocab 128256, RMSNorm eps 1e-5,
+RoPE theta 500000, untied embeddings.
+
+MI355X choices: projections are fused (QKV one GEMM, gate+up one GEMM) so
+hipBLASLt sees fewer, larger MFMA GEMMs; attention goes through
+scaled_dot_product_attention (flash kernels on ROCm); weights are created
+directly on the GPU in bf16 (no CPU materialisation of 16 GB).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 128256
+    d_model: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    ffn_dim: int = 14336
+    norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    max_seq_len: int = 8192
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_model // self.n_heads
+
+    def num_params(self) -> int:
+        d, f, v, L = self.d_model, self.ffn_dim, self.vocab_size, self.n_layers
+        kv = self.n_kv_heads * self.head_dim
+        per_layer = d * (d + 2 * kv) + d * d + 2 * d * f + f * d + 2 * d
+        return L * per_layer + 2 * v * d + d
+
+
+CONFIGS = {
+    "llama3-8b": LlamaConfig(),
+    "llama3-70b": LlamaConfig(d_model=8192, n_layers=80, n_heads=64, n_kv_heads=8,
+                              ffn_dim=28672),
+    # tiny config for CPU unit tests only (never used for reported numbers)
+    "tiny": LlamaConfig(vocab_size=512, d_model=128, n_layers=2, n_heads=4, n_kv_heads=2,
+                        ffn_dim=256, max_seq_len=256),
+}
+
+
+def rope_tables(cfg: LlamaConfig, seq_len: int, device, dtype):
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, cfg.head_dim, 2, device=device,
+                                                 dtype=torch.float32) / cfg.head_dim))
+    t = torch.arange(seq_len, device=device, dtype=torch.float32)
+    f = torch.outer(t, inv)
+    return f.cos().to(dtype), f.sin().to(dtype)
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    # x: [b, h, s, hd]; rotate-half convention (HF Llama)
+    h = x.shape[-1] // 2
+    x1, x2 = x[..., :h], x[..., h:]
+    return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        hd = cfg.head_dim
+        self.wqkv = nn.Linear(cfg.d_model, (cfg.n_heads + 2 * cfg.n_kv_heads) * hd, bias=False)
+        self.wo = nn.Linear(cfg.n_heads * hd, cfg.d_model, bias=False)
+
+    def forward(self, x, cos, sin):
+        b, s, _ = x.shape
+        c = self.cfg
+        hd = c.head_dim
+        q, k, v = self.wqkv(x).split([c.n_heads * hd, c.n_kv_heads * hd, c.n_kv_heads * hd], -1)
+        q = q.view(b, s, c.n_heads, hd).transpose(1, 2)
+        k = k.view(b, s, c.n_kv_heads, hd).transpose(1, 2)
+        v = v.view(b, s, c.n_kv_heads, hd).transpose(1, 2)
+        q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True,
+                                           enable_gqa=c.n_kv_heads != c.n_heads)
+        return self.wo(o.transpose(1, 2).reshape(b, s, c.n_heads * hd))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.w13 = nn.Linear(cfg.d_model, 2 * cfg.ffn_dim, bias=False)
+        self.w2 = nn.Linear(cfg.ffn_dim, cfg.d_model, bias=False)
+
+    def forward(self, x):
+        g, u = self.w13(x).chunk(2, dim=-1)
+        return self.w2(F.silu(g) * u)
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.attn_norm = nn.RMSNorm(cfg.d_model, eps=cfg.norm_eps)
+        self.attn = Attention(cfg)
+        self.ffn_norm = nn.RMSNorm(cfg.d_model, eps=cfg.norm_eps)
+        self.ffn = FeedForward(cfg)
+
+    def forward(self, x, cos, sin):
+        x = x + self.attn(self.attn_norm(x), cos, sin)
+        return x + self.ffn(self.ffn_norm(x))
+
+
+class Llama(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.tok_emb = nn.Embedding(cfg.vocab_size, cfg.d_model)
+        self.layers = nn.ModuleList(Block(cfg) for _ in range(cfg.n_layers))
+        self.norm = nn.RMSNorm(cfg.d_model, eps=cfg.norm_eps)
+        self.head = nn.Linear(cfg.d_model, cfg.vocab_size, bias=False)
+        self._rope = None
+
+    @torch.no_grad()
+    def reset_parameters(self, seed: int = 0) -> None:
+        g = torch.Generator(device=self.head.weight.device).manual_seed(seed)
+        std = 0.02
+        for name, p in self.named_parameters():
+            if p.dim() == 1:
+                p.fill_(1.0)
+            else:
+                p.normal_(0.0, std, generator=g)
+                if name.endswith("wo.weight") or name.endswith("w2.weight"):
+                    p.mul_(1.0 / math.sqrt(2 * self.cfg.n_layers))
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        s = ids.shape[1]
+        if self._rope is None or self._rope[0].shape[0] < s or self._rope[0].device != ids.device:
+            self._rope = rope_tables(self.cfg, max(s, 1), ids.device, self.head.weight.dtype)
+        cos, sin = self._rope[0][:s], self._rope[1][:s]
+        x = self.tok_emb(ids)
+        for layer in self.layers:
+            x = layer(x, cos, sin)
+        return self.head(self.norm(x))
+
+
+def build_llama(name: str = "llama3-8b", device="cuda", dtype=torch.bfloat16,
+                seed: int = 0) -> Llama:
+    """Random-init model created directly on `device` (meta -> to_empty)."""
+    cfg = CONFIGS[name]
+    with torch.device("meta"):
+        m = Llama(cfg)
+    m = m.to_empty(device=device).to(dtype)
+    m.reset_parameters(seed)
+    return m
+
+
+def lm_loss(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1))
