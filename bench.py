@@ -47,6 +47,10 @@ def parse_args(argv=None):
     p.add_argument("--skip-baseline", action="store_true")
     p.add_argument("--log-file", default="", help="agent log destination (default stderr)")
     p.add_argument("--json-out", default="", help="also write the result line here")
+    p.add_argument("--sweep-hz", default="",
+                   help="after the headline run, time K steps at each of these rates "
+                        "(comma list, 0 = free-running) -> --sweep-out")
+    p.add_argument("--sweep-out", default="", help="JSON file for the --sweep-hz table")
     return p.parse_args(argv)
 
 
@@ -148,6 +152,14 @@ def main(argv=None) -> int:
             per_rank = ag.window_counts(m0, m1)
             total_samples = sum(per_rank)
             agent_stats = ag.stats()
+        if base_s is not None:
+            # second baseline AFTER the measured window: the overhead compares
+            # against the mean of the two, cancelling clock/thermal drift.
+            ag.pause()
+            time.sleep(0.05)
+            base2_s, _, _ = timed(args.steps)
+            ag.resume()
+            base_s = 0.5 * (base_s + base2_s)
 
     window_s = (m1 - m0) * 1e-9 if ag is not None else meas_s
     value = total_samples / window_s if window_s > 0 else 0.0
@@ -189,6 +201,35 @@ def main(argv=None) -> int:
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if ag is not None and args.sweep_hz:
+        # Overhead / rate curve (written to --sweep-out, never to stdout):
+        # for each rate, K timed steps with sampling at that rate.
+        sweep = []
+        for hz in [float(h) for h in args.sweep_hz.split(",") if h.strip()]:
+            ag.set_rate(hz)
+            for _ in range(2):
+                train_step()
+            torch.cuda.synchronize()
+            s, a0, a1 = timed(args.steps)
+            ag.pack_pending()
+            pdist.barrier()
+            ag.step()
+            torch.cuda.synchronize()
+            pdist.barrier()
+            n = 0
+            if env.rank == 0:
+                ag.flush()
+                n = sum(ag.window_counts(a0, a1))
+            row = {"sample_hz_target": hz, "ms_per_step": round(s / args.steps * 1e3, 3),
+                   "overhead_pct": round((s / base_s - 1.0) * 100.0, 3) if base_s else None,
+                   "samples_per_sec_per_gpu": round(n / ((a1 - a0) * 1e-9) / env.world, 2)}
+            sweep.append(row)
+            if env.rank == 0:
+                print("sweep", json.dumps(row), file=sys.stderr, flush=True)
+        if env.rank == 0 and args.sweep_out:
+            with open(args.sweep_out, "w") as f:
+                json.dump({"baseline_ms_per_step": out["baseline_ms_per_step"], "rows": sweep}, f,
+                          indent=1)
     if ag is not None:
         ag.stop()
     pdist.shutdown()

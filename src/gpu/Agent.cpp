@@ -279,7 +279,7 @@ bool Agent::flushBatch(int nstaged, std::string* err) {
 
 void Agent::samplerLoop() {
   hipSetDevice(cfg_.device);
-  const uint64_t period = static_cast<uint64_t>(1e9 / std::max(1.0, cfg_.sampleHz));
+  periodNs_ = static_cast<uint64_t>(1e9 / std::max(1.0, cfg_.sampleHz));
   uint64_t next = monoNs();
   int staged = 0;
   std::string err;
@@ -344,6 +344,7 @@ void Agent::samplerLoop() {
         staged = 0;
       }
     }
+    const uint64_t period = periodNs_.load(std::memory_order_relaxed);
     next += period;
     const uint64_t now = monoNs();
     if (now < next) {
@@ -512,6 +513,12 @@ void Agent::packPending() {
   const uint64_t want = ++flushReq_;
   const uint64_t deadline = monoNs() + 2000000000ull;
   while (flushAck_.load() < want && monoNs() < deadline && !paused_) usleep(200);
+}
+
+void Agent::setSampleHz(double hz) {
+  // 0 (or less) = as fast as the device counting service returns samples
+  periodNs_ = hz > 0 ? static_cast<uint64_t>(1e9 / hz) : 1;
+  cfg_.sampleHz = hz;
 }
 
 void Agent::pause() { paused_ = true; }

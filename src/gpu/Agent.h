@@ -80,6 +80,7 @@ class Agent {
   void packPending();
   void pause();
   void resume();
+  void setSampleHz(double hz);
   void stop();
   bool running() const { return running_; }
 
@@ -106,6 +107,7 @@ class Agent {
   std::atomic<bool> paused_{false};
   std::atomic<bool> resetPrev_{false};
   std::atomic<uint64_t> flushReq_{0}, flushAck_{0};
+  std::atomic<uint64_t> periodNs_{1000000};
   std::thread samplerThread_, consumerThread_;
 
   // device buffers

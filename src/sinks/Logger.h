@@ -53,6 +53,7 @@ class JsonLogger : public Logger {
 
  protected:
   const Json& sample() const { return json_; }
+  Json& mutableSample() { return json_; }
   void clearSample() { json_ = Json::object(); }
   std::string timestampStr() const { return isoTimestamp(ts_); }
   Timestamp ts_{};

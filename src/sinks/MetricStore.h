@@ -37,6 +37,11 @@ class StoreLogger : public JsonLogger {
  public:
   StoreLogger(std::shared_ptr<MetricStore> store, std::string collector)
       : store_(std::move(store)), collector_(std::move(collector)) {}
+  // Stored records keep floats numeric (the glog JSON sink formats them as
+  // "%.3f" strings for reference compatibility; the query API does not).
+  void logFloat(const std::string& key, float val) override {
+    mutableSample()[key] = static_cast<double>(val);
+  }
   void finalize() override;
 
  private:
