@@ -68,7 +68,12 @@ def main(argv=None) -> int:
     use_agent = not args.no_agent
     if use_agent:
         from dynolog_amd import agent as dagent
-        dagent.preinit()  # rocprofiler-sdk tool registration: before HIP init
+        # rocprofiler-sdk tool registration: before HIP init. Only this rank's
+        # GPU gets a counting context (agent index == LOCAL_RANK when every GPU
+        # is visible, as under torchrun on one node).
+        visible = any(os.environ.get(v) for v in
+                      ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"))
+        dagent.preinit(None if visible else [int(os.environ.get("LOCAL_RANK", "0"))])
 
     import torch
     from dynolog_amd.models.llama import CONFIGS, build_llama, lm_loss
