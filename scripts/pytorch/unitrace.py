@@ -50,8 +50,18 @@ def slurm_hosts(job_id: str) -> List[str]:
 def expand_hostlist(spec: str) -> List[str]:
     """Minimal hostlist expansion for --hosts: 'n[01-03],x' -> n01,n02,n03,x."""
     hosts = []
-    for part in re.findall(r"[^,\[]+(?:\[[^\]]*\])?", spec):
-        part = part.strip(",")
+    parts, depth, cur = [], 0, ""
+    for ch in spec:  # split on commas outside brackets
+        if ch == "," and depth == 0:
+            parts.append(cur)
+            cur = ""
+            continue
+        depth += ch == "["
+        depth -= ch == "]"
+        cur += ch
+    parts.append(cur)
+    for part in parts:
+        part = part.strip()
         m = re.match(r"^(.*)\[([^\]]+)\](.*)$", part)
         if not m:
             if part:
