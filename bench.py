@@ -43,6 +43,7 @@ def parse_args(argv=None):
     p.add_argument("--sample-hz", type=float, default=1000.0)
     p.add_argument("--pack-batch", type=int, default=32)
     p.add_argument("--gather-mode", default="gather", choices=["gather", "allgather", "none"])
+    p.add_argument("--counter-set", default="full", help="full | lite | core | comma list")
     p.add_argument("--no-agent", action="store_true", help="run the workload only")
     p.add_argument("--skip-baseline", action="store_true")
     p.add_argument("--log-file", default="", help="agent log destination (default stderr)")
@@ -98,6 +99,7 @@ def main(argv=None) -> int:
         ag = dagent.GpuAgent.start(device=env.local_rank, rank=env.rank, world=env.world,
                                    sample_hz=args.sample_hz, batch=args.pack_batch,
                                    gather_mode=args.gather_mode, log_file=args.log_file,
+                                   counter_set=args.counter_set,
                                    sinks=("json", "memory"))
 
     last_loss = [0.0]
@@ -185,7 +187,7 @@ def main(argv=None) -> int:
         "config": {
             "model": args.model, "global_batch": B * env.world, "seq_len": S,
             "parallelism": f"dp{env.world}", "sample_hz_target": args.sample_hz,
-            "counters": 14, "gather": args.gather_mode, "pack_batch": args.pack_batch,
+            "counter_set": args.counter_set, "gather": args.gather_mode, "pack_batch": args.pack_batch,
         },
         "samples_per_sec_per_gpu": round(value / env.world, 3),
         "samples_per_rank": per_rank,

@@ -58,6 +58,7 @@ AgentConfig AgentConfig::fromJson(const Json& j) {
   gi("log_interval_ms", c.logIntervalMs);
   gi("memory_records", c.memoryRecords);
   if (j.contains("gather_mode")) c.gatherMode = j.at("gather_mode").asString();
+  if (j.contains("counter_set")) c.counterSet = j.at("counter_set").asString();
   if (j.contains("log_file")) c.logFile = j.at("log_file").asString();
   if (j.contains("sinks")) {
     c.sinks.clear();
@@ -97,7 +98,7 @@ bool Agent::setupLayout(const std::vector<uint64_t>& ids, std::string* err) {
     for (size_t i = 0; i < counterOf.size(); ++i)
       if (counterOf[i] == c) perm.push_back(static_cast<int>(i));
     segLen[c] = static_cast<int>(perm.size()) - segStart[c];
-    if (segLen[c] == 0) {
+    if (segLen[c] == 0 && !counterNames_[static_cast<size_t>(c)].empty()) {
       *err = "counter " + defaultCounterNames()[c] + " produced no records";
       return false;
     }
@@ -140,9 +141,14 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     }
     if (agentIdx < 0) agentIdx = cfg_.device;
   }
-  sampler_ = std::make_unique<CounterSampler>(agentIdx, defaultCounterNames());
+  counterNames_ = counterNamesForSet(cfg_.counterSet, err);
+  if (counterNames_.empty()) return false;
+  sampler_ = std::make_unique<CounterSampler>(agentIdx, counterNames_);
   if (!sampler_->setup(err)) return false;
   consts_ = makeAgentConsts(sampler_->agent());
+  // Without the size-class counters, price requests by the dominant gfx950
+  // class: 64-B writes (>99.9% of WRREQ in the Llama step, profiles/round1).
+  if (counterNames_[DC_TCC_EA0_WRREQ_64B].empty()) consts_.hbm_write_bytes_per_req = 64.0f;
   R_ = sampler_->rawCount();
 
   int least = 0, greatest = 0;
@@ -558,6 +564,13 @@ Json Agent::stats() const {
   j["sample_latency_us_avg"] = n ? latencySumNs_.load() / static_cast<double>(n) * 1e-3 : 0.0;
   j["sample_latency_us_max"] = latencyMaxNs_.load() * 1e-3;
   j["raw_instances"] = static_cast<unsigned long long>(R_);
+  j["counter_set"] = cfg_.counterSet;
+  {
+    Json names = Json::array();
+    for (const auto& n : counterNames_)
+      if (!n.empty()) names.push_back(n);
+    j["counters"] = names;
+  }
   j["elapsed_s"] = running_ ? (monoNs() - startNs_) * 1e-9 : 0.0;
   j["last_error"] = lastError_;
   if (sampler_) j["agent"] = sampler_->agent().name;

@@ -54,6 +54,40 @@ const std::vector<std::string>& defaultCounterNames() {
   return names;
 }
 
+std::vector<std::string> counterNamesForSet(const std::string& set, std::string* err) {
+  std::vector<std::string> names = defaultCounterNames();
+  auto disable = [&](std::initializer_list<int> slots) {
+    for (int s : slots) names[static_cast<size_t>(s)].clear();
+  };
+  if (set.empty() || set == "full") return names;
+  if (set == "lite") {
+    disable({DC_TCC_EA0_RDREQ_32B, DC_TCC_EA0_WRREQ_64B});
+    return names;
+  }
+  if (set == "core") {
+    disable({DC_TCC_EA0_RDREQ, DC_TCC_EA0_WRREQ, DC_TCC_EA0_WRREQ_64B, DC_TCC_EA0_RDREQ_32B});
+    return names;
+  }
+  // explicit list
+  std::vector<std::string> out(names.size());
+  size_t start = 0;
+  while (start <= set.size()) {
+    size_t comma = set.find(',', start);
+    std::string n = set.substr(start, comma == std::string::npos ? std::string::npos : comma - start);
+    if (!n.empty()) {
+      auto it = std::find(names.begin(), names.end(), n);
+      if (it == names.end()) {
+        if (err) *err = "unknown counter '" + n + "' (canonical set: see defaultCounterNames)";
+        return {};
+      }
+      out[static_cast<size_t>(it - names.begin())] = n;
+    }
+    if (comma == std::string::npos) break;
+    start = comma + 1;
+  }
+  return out;
+}
+
 const std::vector<std::string>& derivedMetricNames() {
   static const std::vector<std::string> names = {
       "gpu_busy_pct",  "mfma_util",     "mfma_bf16_tflops",  "hbm_read_gbps",
@@ -257,6 +291,7 @@ bool CounterSampler::setup(std::string* err) {
   std::vector<rocprofiler_counter_id_t> want;
   expected_ = 0;
   for (size_t i = 0; i < counters_.size(); ++i) {
+    if (counters_[i].empty()) continue;  // slot disabled in this counter set
     auto it = byName.find(counters_[i]);
     if (it == byName.end()) {
       *err = "counter " + counters_[i] + " not supported on " + agent_.name;

@@ -110,6 +110,15 @@ class CounterSampler {
 };
 
 const std::vector<std::string>& defaultCounterNames();
+// Counter sets trade detail for per-sample cost (the command processor reads
+// every instance register of every counter on each sample; ~0.4-0.6 us per
+// instance measured, profiles/round1/counter_set_latency.md):
+//   full    14 counters, 784 instances on MI355X
+//   lite    drops TCC_EA0_RDREQ_32B / TCC_EA0_WRREQ_64B (528 instances)
+//   core    SQ + GRBM only, no HBM traffic (272 instances)
+//   or a comma list of canonical counter names.
+// Returns DynoCounter-ordered names with "" for disabled slots.
+std::vector<std::string> counterNamesForSet(const std::string& set, std::string* err);
 const std::vector<std::string>& derivedMetricNames();
 DynoAgentConsts makeAgentConsts(const AgentInfo& a);
 
