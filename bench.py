@@ -5,17 +5,20 @@ Llama-3-8B DDP training step (BASELINE.json metric / config).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (driver does this for N>1)
 
-Per rank: the in-process agent samples 14 SQ/TCC/GRBM counters of its
-MI355X through rocprofiler-sdk device counting at --sample-hz, packs them
-with the CDNA4 sampler_pack kernel into an HBM ring, and every training step
-gathers the new slots to rank 0 over RCCL (ncclGather, xGMI).  Rank 0 drains
-them over PCIe, aggregates per GPU and logs through the Logger sinks.
+Per rank: the in-process agent samples the SQ/TCC/GRBM counters of its
+MI355X (--counter-set lite: 12 counters, 528 instances) through
+rocprofiler-sdk device counting at --sample-hz, packs them with the CDNA4
+sampler_pack kernel into an HBM ring, and every training step gathers the
+new slots to rank 0 over RCCL (ncclGather, xGMI).  Rank 0 drains them over
+PCIe, aggregates per GPU and logs through the Logger sinks.
 
 Timed phases (each bracketed by barrier + cuda.synchronize, max over ranks):
   1. baseline: K steps with the agent paused (no sampling, no gathers)
   2. measured: K steps with sampling + per-step gather   -> ms_per_step
+  3. baseline again, then --ab-rounds interleaved paused/sampling windows
 value = counter samples (taken inside phase 2's window and delivered to
-rank 0) / window seconds, summed over all GPUs.  overhead % = phase2/phase1-1.
+rank 0) / window seconds, summed over all GPUs.  tracing_overhead_pct =
+pooled sampling ms/step (phases 2+3) / pooled paused ms/step (1+3) - 1.
 Data: synthetic random tokens; weights: random init of the full Llama-3-8B.
 """
 from __future__ import annotations
@@ -43,9 +46,12 @@ def parse_args(argv=None):
     p.add_argument("--sample-hz", type=float, default=1000.0)
     p.add_argument("--pack-batch", type=int, default=32)
     p.add_argument("--gather-mode", default="gather", choices=["gather", "allgather", "none"])
-    p.add_argument("--counter-set", default="full", help="full | lite | core | comma list")
+    p.add_argument("--counter-set", default="lite", help="lite (default) | full | core | comma list")
     p.add_argument("--no-agent", action="store_true", help="run the workload only")
     p.add_argument("--skip-baseline", action="store_true")
+    p.add_argument("--ab-rounds", type=int, default=4,
+                   help="interleaved paused/sampling window pairs for the overhead estimate")
+    p.add_argument("--ab-steps", type=int, default=5, help="steps per A/B window")
     p.add_argument("--log-file", default="", help="agent log destination (default stderr)")
     p.add_argument("--json-out", default="", help="also write the result line here")
     p.add_argument("--sweep-hz", default="",
@@ -132,6 +138,7 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
 
     base_s = None
+    pooled_active_s = None
     if ag is not None and not args.skip_baseline:
         ag.pause()
         time.sleep(0.05)
@@ -160,13 +167,32 @@ def main(argv=None) -> int:
             total_samples = sum(per_rank)
             agent_stats = ag.stats()
         if base_s is not None:
-            # second baseline AFTER the measured window: the overhead compares
-            # against the mean of the two, cancelling clock/thermal drift.
+            # second baseline AFTER the measured window, then --ab-rounds of
+            # interleaved (paused, sampling) window pairs in alternating order.
+            # MI355X sclk swings ~5% under its power cap (visible in the
+            # agent's own sclk_mhz), so a single A/B pair cannot resolve a
+            # sub-1% overhead; pooling all windows can.
             ag.pause()
             time.sleep(0.05)
             base2_s, _, _ = timed(args.steps)
+            paused_s, paused_n = base_s + base2_s, 2 * args.steps
+            active_s, active_n = meas_s, args.steps
+            for r in range(args.ab_rounds):
+                for want_active in ((True, False) if r % 2 == 0 else (False, True)):
+                    if want_active:
+                        ag.resume()
+                        train_step()
+                        torch.cuda.synchronize()
+                        s, _, _ = timed(args.ab_steps)
+                        active_s, active_n = active_s + s, active_n + args.ab_steps
+                        ag.pause()
+                        time.sleep(0.02)
+                    else:
+                        s, _, _ = timed(args.ab_steps)
+                        paused_s, paused_n = paused_s + s, paused_n + args.ab_steps
             ag.resume()
-            base_s = 0.5 * (base_s + base2_s)
+            base_s = paused_s / paused_n * args.steps
+            pooled_active_s = active_s / active_n * args.steps
 
     window_s = (m1 - m0) * 1e-9 if ag is not None else meas_s
     value = total_samples / window_s if window_s > 0 else 0.0
@@ -192,7 +218,10 @@ def main(argv=None) -> int:
         "samples_per_sec_per_gpu": round(value / env.world, 3),
         "samples_per_rank": per_rank,
         "baseline_ms_per_step": round(base_s / args.steps * 1e3, 3) if base_s else None,
-        "tracing_overhead_pct": round((meas_s / base_s - 1.0) * 100.0, 3) if base_s else None,
+        # pooled over the headline window + every interleaved A/B window
+        "tracing_overhead_pct": round((pooled_active_s / base_s - 1.0) * 100.0, 3) if base_s else None,
+        "overhead_pct_headline_window": round((meas_s / base_s - 1.0) * 100.0, 3) if base_s else None,
+        "ab_windows": {"steps": args.ab_steps, "rounds": args.ab_rounds} if base_s else None,
         "tokens_per_sec": round(tokens / meas_s, 1),
         "loss": round(loss_val, 4),
         "vs_baseline_note": "value / (0.1 samples/s/GPU x n_gpus): reference DCGM 10 s interval",

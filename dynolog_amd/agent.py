@@ -77,7 +77,7 @@ class GpuAgent:
     @classmethod
     def start(cls, device: int = 0, rank: int = 0, world: int = 1,
               sample_hz: float = 1000.0, batch: int = 32, ring_slots: int = 1 << 20,
-              gather_cap_slots: int = 4096, gather_mode: str = "gather", counter_set: str = "full",
+              gather_cap_slots: int = 4096, gather_mode: str = "gather", counter_set: str = "lite",
               log_interval_ms: int = 1000, sinks: Sequence[str] = ("json",),
               log_file: str = "", uid: Optional[bytes] = None, process_group=None) -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is

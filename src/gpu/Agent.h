@@ -45,7 +45,7 @@ struct AgentConfig {
   uint64_t ringSlots = 1ull << 20;   // 256 MiB of HBM history per GPU
   uint32_t gatherCapSlots = 4096;    // max slots per rank per gather (1 MiB)
   std::string gatherMode = "gather"; // gather | allgather | none
-  std::string counterSet = "full";   // full | lite | core | comma list (RocprofSampler.h)
+  std::string counterSet = "lite";   // full | lite | core | comma list (RocprofSampler.h)
   int logIntervalMs = 1000;
   std::vector<std::string> sinks = {"json"};  // json | memory | prometheus | none
   std::string logFile;               // redirect daemon-style log lines
