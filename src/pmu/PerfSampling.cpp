@@ -429,6 +429,23 @@ int ringCountFor(const CpuSet& cpus) {
   int n = std::max(cpus.empty() ? 0 : cpus.last() + 1, all.empty() ? 1 : all.last() + 1);
   return std::max(n, 1);
 }
+
+// Per-task events cannot be inherited *and* mmapped (the kernel refuses to
+// mmap an inherited cpu=-1 event), so a process target is followed by one
+// event group per existing thread.
+std::vector<int> listTasks(int pid) {
+  std::vector<int> tids;
+  const std::string dir = "/proc/" + std::to_string(pid) + "/task";
+  if (DIR* d = opendir(dir.c_str())) {
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] >= '0' && e->d_name[0] <= '9') tids.push_back(atoi(e->d_name));
+    }
+    closedir(d);
+  }
+  std::sort(tids.begin(), tids.end());
+  if (tids.empty()) tids.push_back(pid);
+  return tids;
+}
 }  // namespace
 
 class CountSampleGenerator::Handler : public RecordHandler {
@@ -477,7 +494,8 @@ CountSampleGenerator::CountSampleGenerator(const CpuSet& cpus, Target target,
     if (target.cgroupFd >= 0) {
       for (int c : cpus.cpus()) groups_.push_back(std::make_unique<SamplingGroup>(c, target, events, conf));
     } else {
-      groups_.push_back(std::make_unique<SamplingGroup>(-1, target, events, conf));
+      for (int tid : listTasks(target.pid))
+        groups_.push_back(std::make_unique<SamplingGroup>(-1, Target::process(tid), events, conf));
     }
   } else {
     for (int c : cpus.cpus()) groups_.push_back(std::make_unique<SamplingGroup>(c, target, events, conf));
@@ -511,10 +529,11 @@ size_t CountSampleGenerator::poll() {
   return n;
 }
 
-size_t CountSampleGenerator::accumUntil(int64_t stopTs, const std::function<void(const CountSample&)>& fn) {
+size_t CountSampleGenerator::accumUntil(int64_t stopTs, const std::function<void(const CountSample&)>& fn,
+                                        size_t maxSamples) {
   size_t n = 0;
-  for (size_t c = 0; c < consumers_.size(); ++c) {
-    while (true) {
+  for (size_t c = 0; c < consumers_.size() && n < maxSamples; ++c) {
+    while (n < maxSamples) {
       if (!peeked_[c]) {
         CountSample s;
         if (consumers_[c]->read(&s) < 0) break;
@@ -595,21 +614,6 @@ class ThreadSwitchGenerator::Handler : public RecordHandler {
   ThreadSwitchGenerator* g_;
   int ring_;
 };
-
-namespace {
-std::vector<int> listTasks(int pid) {
-  std::vector<int> tids;
-  const std::string dir = "/proc/" + std::to_string(pid) + "/task";
-  if (DIR* d = opendir(dir.c_str())) {
-    while (dirent* e = readdir(d)) {
-      if (e->d_name[0] >= '0' && e->d_name[0] <= '9') tids.push_back(atoi(e->d_name));
-    }
-    closedir(d);
-  }
-  std::sort(tids.begin(), tids.end());
-  return tids;
-}
-}  // namespace
 
 ThreadSwitchGenerator::ThreadSwitchGenerator(const CpuSet& cpus, Target target, uint64_t ringBytesPerCpu)
     : cpus_(cpus), target_(target),

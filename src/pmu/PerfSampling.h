@@ -208,7 +208,8 @@ class CountSampleGenerator {
   size_t poll();
   // Reference accumUntil (PerCpuSampleGeneratorBase.h:47-99): consume the
   // buffered samples with tstamp <= stopTs, oldest first per CPU.
-  size_t accumUntil(int64_t stopTs, const std::function<void(const CountSample&)>& fn);
+  size_t accumUntil(int64_t stopTs, const std::function<void(const CountSample&)>& fn,
+                    size_t maxSamples = SIZE_MAX);
   uint64_t dropped() const { return dropped_; }
   uint64_t lost() const { return lost_; }
   size_t numGroups() const { return groups_.size(); }

@@ -7,7 +7,7 @@ import pytest
 
 SUITES = ["Json", "Flags", "System", "KernelCollector", "Sinks", "SmiMonitor", "Rpc",
           "KinetoConfigManager", "IpcFabric", "IpcMonitor", "Pmu", "MetricFrame",
-          "RingBuffer", "TagStack", "PerfSampling"]
+          "RingBuffer", "TagStack", "PerfSampling", "Mon"]
 
 
 @pytest.mark.parametrize("suite", SUITES)
