@@ -9,6 +9,7 @@
 #include "common/Flags.h"
 #include "common/Logging.h"
 #include "common/System.h"
+#include "daemon/CpuTrace.h"
 #include "daemon/Daemon.h"
 #include "pmu/PerfMonitor.h"
 #include "rpc/RpcServer.h"
@@ -139,6 +140,7 @@ void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d) {
     j["active"] = gPerf ? Json(gPerf->activeMetrics()) : Json::array();
     return j;
   });
+  disp.add("cpuTrace", [](const Json& req) -> std::optional<Json> { return runCpuTrace(req); });
   (void)d;
 }
 

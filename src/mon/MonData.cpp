@@ -50,7 +50,7 @@ void TagStackIdBinner::addSlice(const Slice& s) {
   durations_[s.stackId] += s.duration;
 }
 
-bool TagStackIdBinner::addSample(CompUnitId cu, TimeStamp t, const double* values) {
+bool TagStackIdBinner::addSample(CompUnitId cu, TimeStamp t, const double* values, TagStackId fallback) {
   TagStackId id = tagstack::kInvalidTagStackId;
   auto uit = slices_.find(cu);
   if (uit != slices_.end()) {
@@ -61,14 +61,13 @@ bool TagStackIdBinner::addSample(CompUnitId cu, TimeStamp t, const double* value
       if (t <= it->second.tstamp + it->second.duration) id = it->second.stackId;
     }
   }
+  const bool covered = id != tagstack::kInvalidTagStackId;
+  if (!covered) id = fallback;
   auto& tot = totals_[id];
   if (tot.empty()) tot.assign(ncols_, 0.0);
   for (size_t i = 0; i < ncols_; ++i) tot[i] += values[i];
-  if (id == tagstack::kInvalidTagStackId) {
-    ++unattributed_;
-    return false;
-  }
-  return true;
+  if (id == tagstack::kInvalidTagStackId) ++unattributed_;
+  return covered;
 }
 
 // ------------------------------------------------------------------ MonData

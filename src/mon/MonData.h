@@ -79,8 +79,10 @@ class TagStackIdBinner {
  public:
   explicit TagStackIdBinner(size_t numCols) : ncols_(numCols) {}
   void addSlice(const Slice& s);
-  // false if no slice covers (cu, t): counted under kInvalidTagStackId
-  bool addSample(CompUnitId cu, TimeStamp t, const double* values);
+  // false if no slice covers (cu, t): counted under `fallback`
+  // (kInvalidTagStackId unless the caller knows better, e.g. the sample's tid).
+  bool addSample(CompUnitId cu, TimeStamp t, const double* values,
+                 TagStackId fallback = tagstack::kInvalidTagStackId);
   const std::map<TagStackId, std::vector<double>>& totals() const { return totals_; }
   const std::map<TagStackId, TimeStamp>& durations() const { return durations_; }
   uint64_t unattributed() const { return unattributed_; }

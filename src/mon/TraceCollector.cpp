@@ -71,11 +71,18 @@ void TraceCollector::collectUntil(TimeStamp t) {
   if (switches_) switches_->poll();
   if (counts_) counts_->poll();
   std::lock_guard<std::mutex> lk(mu_);
-  if (comb_) tagstack::drain(*comb_, *slicer_, t);
+  if (comb_) {
+    tagstack::drain(*comb_, *slicer_, t);
+    // close the running slices at t so long-running threads show up now
+    slicer_->flush(t);
+  }
   if (counts_) {
     counts_->accumUntil(t, [&](const pmu::CountSample& s) {
       data_.addSample(static_cast<CompUnitId>(s.cpu), s.tstamp, s.deltas, s.numEvents);
-      binner_.addSample(static_cast<CompUnitId>(s.cpu), s.tstamp, s.deltas);
+      // a thread already on-CPU when tracing began has no switch-in yet: its
+      // samples still carry the tid, i.e. the thread's base tag stack
+      const TagStackId fallback = s.tid ? slicer_->intern(tagstack::Stack{{s.tid}}) : tagstack::kInvalidTagStackId;
+      binner_.addSample(static_cast<CompUnitId>(s.cpu), s.tstamp, s.deltas, fallback);
       if (binMatrix_) binMatrix_->add(s.tstamp, s.deltas);
     });
   }
@@ -161,13 +168,20 @@ Json TraceCollector::summary(size_t topN) const {
   auto t = data_.total();
   for (size_t i = 0; i < columns_.size() && i < t.size(); ++i) tot[columns_[i]] = t[i];
   j["totals"] = tot;
-  // tag stacks ranked by time
+  // tag stacks ranked by sliced time, then by the leading count column
+  // (stacks seen only through samples have no slices yet)
+  const auto& counts = binner_.totals();
+  std::map<TagStackId, std::pair<TimeStamp, double>> keys;
+  for (const auto& [id, d] : binner_.durations()) keys[id].first = d;
+  for (const auto& [id, c] : counts)
+    if (id != tagstack::kInvalidTagStackId) keys[id].second = c.empty() ? 0.0 : c[0];
+  std::vector<std::pair<std::pair<TimeStamp, double>, TagStackId>> ranked;
+  for (const auto& [id, k] : keys) ranked.emplace_back(k, id);
+  std::sort(ranked.rbegin(), ranked.rend());
   std::vector<std::pair<TimeStamp, TagStackId>> order;
-  for (const auto& [id, d] : binner_.durations()) order.emplace_back(d, id);
-  std::sort(order.rbegin(), order.rend());
+  for (const auto& [k, id] : ranked) order.emplace_back(k.first, id);
   Json stacks = Json::array();
   const auto& st = slicer_->stackStats();
-  const auto& counts = binner_.totals();
   for (size_t i = 0; i < order.size() && i < topN; ++i) {
     const TagStackId id = order[i].second;
     Json s = Json::object();
