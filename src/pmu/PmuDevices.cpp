@@ -272,6 +272,29 @@ std::optional<EventConf> PmuDeviceManager::resolve(const std::string& specIn, st
   // forms: "name[:mods]", "pmu/fields/[mods]", "pmu:alias[:mods]"
   std::string spec = trim(specIn);
   EventConf e;
+  if (startsWith(spec, "tracepoint:")) {
+    // tracepoint:<subsystem>:<event>; the id comes from tracefs (or the
+    // legacy debugfs mount)
+    auto parts = split(spec.substr(11), ':');
+    if (parts.size() != 2) {
+      if (err) *err = "bad tracepoint spec '" + spec + "' (expected tracepoint:subsys:event)";
+      return std::nullopt;
+    }
+    std::optional<int64_t> id;
+    for (const char* base : {"/sys/kernel/tracing/events/", "/sys/kernel/debug/tracing/events/"}) {
+      id = readInt(root_ + base + parts[0] + "/" + parts[1] + "/id");
+      if (id) break;
+    }
+    if (!id) {
+      if (err) *err = "tracepoint " + parts[0] + ":" + parts[1] + " not found (tracefs not mounted or no access)";
+      return std::nullopt;
+    }
+    e.name = spec;
+    e.type = PERF_TYPE_TRACEPOINT;
+    e.config = static_cast<uint64_t>(*id);
+    e.pmu = "tracepoint";
+    return e;
+  }
   auto slash = spec.find('/');
   if (slash != std::string::npos) {
     auto slash2 = spec.find('/', slash + 1);
