@@ -9,6 +9,7 @@
 #include "common/Flags.h"
 #include "common/Logging.h"
 #include "common/System.h"
+#include "collectors/gpu/Topology.h"
 #include "daemon/CpuTrace.h"
 #include "daemon/Daemon.h"
 #include "pmu/PerfMonitor.h"
@@ -141,6 +142,18 @@ void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d) {
     return j;
   });
   disp.add("cpuTrace", [](const Json& req) -> std::optional<Json> { return runCpuTrace(req); });
+  disp.add("getTopology", [](const Json&) -> std::optional<Json> {
+    gpu::GpuTopology topo;
+    std::string err;
+    if (!gpu::discoverTopology(&topo, &err)) {
+      Json j = Json::object();
+      j["status"] = "failed: " + err;
+      return j;
+    }
+    Json j = topo.toJson();
+    j["status"] = "ok";
+    return j;
+  });
   (void)d;
 }
 

@@ -47,9 +47,11 @@ struct AgentConfig {
   std::string gatherMode = "gather"; // gather | allgather | none
   std::string counterSet = "lite";   // full | lite | core | comma list (RocprofSampler.h)
   int logIntervalMs = 1000;
-  std::vector<std::string> sinks = {"json"};  // json | memory | prometheus | none
+  std::vector<std::string> sinks = {"json"};  // json | memory | prometheus | daemon | none
+  std::string daemonEndpoint = "dynolog";     // IPC endpoint of the node daemon ("daemon" sink)
   std::string logFile;               // redirect daemon-style log lines
   size_t memoryRecords = 4096;
+  bool pinThreads = true;            // sampler/consumer on the GPU's NUMA-local CPUs
 
   static AgentConfig fromJson(const Json& j);
 };
@@ -169,6 +171,7 @@ class Agent {
       gathers_{0}, latencySumNs_{0}, latencyMaxNs_{0}, lateTicks_{0};
   std::string lastError_;
   uint64_t startNs_ = 0;
+  std::string pinnedCpus_;
 };
 
 uint64_t monoNs();

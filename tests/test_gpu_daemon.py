@@ -122,3 +122,55 @@ def test_gputrace_gpu_kernels(native_built, tmp_path):
                     p.kill()
     finally:
         shutil.rmtree(sockdir, ignore_errors=True)
+
+
+def test_agent_forwards_records_to_daemon(native_built):
+    """In-process agent -> node daemon over the IPC fabric ("gmet"): the
+    high-rate per-GPU aggregates show up in the daemon's gpu_counters store."""
+    sockdir = tempfile.mkdtemp(prefix="dy", dir="/tmp")
+    env = {"KINETO_IPC_SOCKET_DIR": sockdir}
+    try:
+        with DaemonProcess(["--enable_ipc_monitor", "--use_JSON"], env=env) as d:
+            code = textwrap.dedent("""
+                from dynolog_amd import agent
+                agent.preinit()
+                import time, torch
+                a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("daemon",),
+                                         log_interval_ms=200)
+                x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+                end = time.time() + 1.5
+                while time.time() < end:
+                    for _ in range(10):
+                        y = x @ x
+                    torch.cuda.synchronize()
+                    a.step()
+                a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+                time.sleep(0.5)
+                a.stop()
+            """)
+            penv = dict(os.environ, KINETO_IPC_SOCKET_DIR=sockdir,
+                        PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            r = subprocess.run([sys.executable, "-c", code], env=penv, capture_output=True,
+                               text=True, timeout=240)
+            assert r.returncode == 0, r.stderr[-4000:]
+            recs = _wait_records(d, "gpu_counters", lambda x: x.get("source") == "agent")
+            agent_recs = [x for x in recs if x.get("source") == "agent"]
+            assert agent_recs, recs
+            rec = agent_recs[-1]
+            assert rec["device"] == 0
+            assert rec["counter_samples"] > 50
+            assert float(rec["mfma_util"]) > 1.0
+    finally:
+        shutil.rmtree(sockdir, ignore_errors=True)
+
+
+def test_topology_rpc(native_built):
+    with DaemonProcess([]) as d:
+        t = d.rpc({"fn": "getTopology"})
+    assert t["status"] == "ok", t
+    assert len(t["gpus"]) >= 1
+    g = t["gpus"][0]
+    assert len(g["bdf"]) == len("0000:05:00.0")
+    assert g["numa_node"] >= 0
+    n = len(t["gpus"])
+    assert len(t["links"]) == n * (n - 1) // 2
