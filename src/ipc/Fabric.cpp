@@ -3,6 +3,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cerrno>
 #include <cstdlib>
 #include <stdexcept>
@@ -61,7 +62,15 @@ std::string Endpoint::nameFromAddress(const sockaddr_un& a, socklen_t len) {
   return std::string(a.sun_path + 1, strnlen(a.sun_path + 1, pathLen - 1));
 }
 
-Endpoint::Endpoint(const std::string& name) : name_(name) {
+Endpoint::Endpoint(const std::string& nameIn) : name_(nameIn) {
+  // Filesystem-socket mode has no autobind: an anonymous endpoint gets a
+  // unique name of its own in $KINETO_IPC_SOCKET_DIR instead.
+  std::string name = nameIn;
+  if (name.empty() && socketDir()) {
+    static std::atomic<uint32_t> seq{0};
+    name = "anon_" + std::to_string(getpid()) + "_" + std::to_string(seq++);
+    name_ = name;
+  }
   fd_ = ::socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC, 0);
   if (fd_ < 0) throw std::runtime_error(std::string("socket: ") + strerror(errno));
   sockaddr_un a;
