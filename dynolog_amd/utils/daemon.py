@@ -51,8 +51,8 @@ class DaemonProcess:
         except OSError:
             return ""
 
-    def rpc(self, req) -> Optional[dict]:
-        return client.call(req, port=self.port)
+    def rpc(self, req, timeout: float = 10.0) -> Optional[dict]:
+        return client.call(req, port=self.port, timeout=timeout)
 
     def stop(self, timeout: float = 10.0) -> int:
         if self.proc is None:

@@ -2,6 +2,8 @@
 
 #include <sys/prctl.h>
 
+#include <algorithm>
+
 #include "collectors/KernelCollector.h"
 #include "collectors/gpu/SmiMonitor.h"
 #include "common/Flags.h"
@@ -89,6 +91,32 @@ bool Daemon::start(std::string* err) {
   handler_->setMetricStore(store_);
   auto dispatcher = rpc::makeDispatcher(handler_);
   registerPluginRpcs(*dispatcher, *this);
+  gpuAgents_ = std::make_shared<tracing::GpuAgentRegistry>();
+  dispatcher->add("getGpuAgents", [this](const Json&) -> std::optional<Json> { return gpuAgents_->listJson(); });
+  // On-demand GPU kernel trace through the in-process agents (IPC "gktr").
+  dispatcher->add("gpuKernelTrace", [this](const Json& req) -> std::optional<Json> {
+    if (!ipc_) {
+      Json j = Json::object();
+      j["status"] = "failed: IPC monitor disabled (start dynolog with --enable_ipc_monitor)";
+      return j;
+    }
+    std::vector<int> pids;
+    if (req.contains("pids") && req.at("pids").isArray())
+      for (const auto& p : req.at("pids").asArray())
+        if (p.isNumber() && p.asInt() > 0) pids.push_back(static_cast<int>(p.asInt()));
+    auto geti = [&](const char* k, int64_t d) {
+      return req.contains(k) && req.at(k).isNumber() ? req.at(k).asInt() : d;
+    };
+    const int dur = static_cast<int>(std::clamp<int64_t>(geti("duration_ms", 500), 10, 60000));
+    const int top = static_cast<int>(std::clamp<int64_t>(geti("top", 20), 1, 500));
+    const std::string dir = req.contains("chrome_dir") && req.at("chrome_dir").isString()
+                                ? req.at("chrome_dir").asString()
+                                : "";
+    return gpuAgents_->kernelTrace(pids, dur, top, dir,
+                                   [this](const std::string& t, const std::string& p, const std::string& d) {
+                                     return ipc_->send(t, p, d);
+                                   });
+  });
   server_ = std::make_unique<rpc::RpcServer>(dispatcher, FLAGS_port, FLAGS_rpc_workers);
   if (!server_->ok()) {
     *err = server_->error();
@@ -103,6 +131,7 @@ bool Daemon::start(std::string* err) {
       *err = "failed to bind IPC endpoint '" + FLAGS_ipc_endpoint + "'";
       return false;
     }
+    ipc_->setAgentRegistry(gpuAgents_);
     // GPU agents inside training processes may forward their per-GPU
     // counter records to the daemon ("gmet" messages).
     ipc_->setMetricsCallback([this](const Json& rec) {

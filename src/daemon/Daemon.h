@@ -34,6 +34,7 @@ class ServiceHandler;
 }  // namespace rpc
 namespace tracing {
 class IpcMonitor;
+class GpuAgentRegistry;
 }
 class PrometheusExporter;
 
@@ -62,6 +63,7 @@ class Daemon {
 
   std::shared_ptr<MetricStore> store_;
   std::shared_ptr<rpc::ServiceHandler> handler_;
+  std::shared_ptr<tracing::GpuAgentRegistry> gpuAgents_;
   std::unique_ptr<rpc::RpcServer> server_;
   std::unique_ptr<tracing::IpcMonitor> ipc_;
   std::unique_ptr<PrometheusExporter> prom_;

@@ -8,8 +8,11 @@
 #include <cstring>
 #include <fstream>
 
+#include <poll.h>
+
 #include "collectors/gpu/Topology.h"
 #include "common/Logging.h"
+#include "gpu/KernelTracer.h"
 #include "ipc/Fabric.h"
 #include "sinks/Prometheus.h"
 
@@ -68,6 +71,8 @@ AgentConfig AgentConfig::fromJson(const Json& j) {
     c.sinks.clear();
     for (const auto& s : j.at("sinks").asArray()) c.sinks.push_back(s.asString());
   }
+  c.daemonControl = std::find(c.sinks.begin(), c.sinks.end(), "daemon") != c.sinks.end();
+  if (j.contains("daemon_control")) c.daemonControl = j.at("daemon_control").asBool();
   return c;
 }
 
@@ -78,8 +83,8 @@ Agent* Agent::instance() {
   return a;
 }
 
-bool Agent::preinit(const std::vector<int>& agentIndices, std::string* err) {
-  return RocprofRuntime::get().preinit(agentIndices, err);
+bool Agent::preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace) {
+  return RocprofRuntime::get().preinit(agentIndices, err, kernelTrace);
 }
 
 namespace {
@@ -301,6 +306,11 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     }
   }
   pinnedCpus_ = pinned;
+  if (cfg_.daemonControl) {
+    ctl_ = ipc::Fabric::create("dynoagent_" + std::to_string(getpid()) + "_r" + std::to_string(cfg_.rank));
+    if (ctl_) ctlThread_ = std::thread([this] { controlLoop(); });
+    else LOG(WARNING) << "GPU agent: daemon control endpoint unavailable";
+  }
   LOG(INFO) << "GPU agent started: rank " << cfg_.rank << "/" << cfg_.world << " device "
             << cfg_.device << " agent " << sampler_->agent().name << " (" << R_
             << " raw counter instances) at " << cfg_.sampleHz << " Hz, batch " << cfg_.batch
@@ -591,12 +601,65 @@ void Agent::setSampleHz(double hz) {
 void Agent::pause() { paused_ = true; }
 void Agent::resume() { paused_ = false; }
 
+// Control channel to the node daemon: periodic "gctx" registration and
+// on-demand kernel traces ("gktr" -> KernelTracer -> "gktd").
+void Agent::controlLoop() {
+  const int pid = static_cast<int>(getpid());
+  uint64_t nextKeepalive = 0;
+  while (!stopFlag_) {
+    const uint64_t now = monoNs();
+    if (now >= nextKeepalive) {
+      Json c = Json::object();
+      c["pid"] = pid;
+      c["rank"] = cfg_.rank;
+      c["device"] = cfg_.device;
+      c["endpoint"] = ctl_->endpoint().name();
+      c["kernel_trace"] = KernelTracer::get().configured();
+      (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgAgentContext, c.dump()), cfg_.daemonEndpoint, 1, 0);
+      nextKeepalive = now + 10'000'000'000ull;
+    }
+    pollfd p{ctl_->endpoint().fd(), POLLIN, 0};
+    if (::poll(&p, 1, 100) <= 0) continue;
+    while (ctl_->recv()) {
+      auto msg = ctl_->retrieve();
+      if (!msg || !msg->typeIs(ipc::kMsgKernelTraceReq)) continue;
+      Json req, res = Json::object();
+      std::string err;
+      if (!Json::tryParse(std::string(msg->buf.begin(), msg->buf.end()), &req, &err)) continue;
+      res["id"] = req.contains("id") ? req.at("id") : Json(0);
+      res["pid"] = pid;
+      res["rank"] = cfg_.rank;
+      res["device"] = cfg_.device;
+      auto& kt = KernelTracer::get();
+      const int dur = req.contains("duration_ms") ? static_cast<int>(req.at("duration_ms").asInt()) : 500;
+      const int top = req.contains("top") ? static_cast<int>(req.at("top").asInt()) : 20;
+      if (!kt.start(&err)) {
+        res["status"] = "failed: " + err;
+      } else {
+        const uint64_t end = monoNs() + static_cast<uint64_t>(dur) * 1000000ull;
+        while (!stopFlag_ && monoNs() < end) usleep(10000);
+        kt.stop(&err);
+        res["status"] = "ok";
+        res["summary"] = kt.summary(static_cast<size_t>(std::max(top, 1)));
+        if (req.contains("chrome_path") && req.at("chrome_path").isString()) {
+          const std::string path = req.at("chrome_path").asString();
+          if (kt.writeChromeTrace(path, &err)) res["chrome_path"] = path;
+          else res["chrome_error"] = err;
+        }
+      }
+      (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, res.dump()), msg->src, 3, 10000);
+    }
+  }
+}
+
 void Agent::stop() {
   if (!running_) return;
   stopFlag_ = true;
   cv_.notify_all();
   if (samplerThread_.joinable()) samplerThread_.join();
   if (consumerThread_.joinable()) consumerThread_.join();
+  if (ctlThread_.joinable()) ctlThread_.join();
+  ctl_.reset();
   sampler_->stop();
   hipSetDevice(cfg_.device);
   hipDeviceSynchronize();

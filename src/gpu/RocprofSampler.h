@@ -47,7 +47,9 @@ class RocprofRuntime {
   // Register our tool. devices: GPU agent indices to create counting
   // contexts for (empty = all).  Must run before HIP init; returns false
   // (with reason) if the runtime is already locked or rocprofiler fails.
-  bool preinit(const std::vector<int>& devices, std::string* err);
+  // kernelTrace: also configure on-demand kernel dispatch tracing
+  // (KernelTracer.h; makes rocprofiler intercept the HSA queues).
+  bool preinit(const std::vector<int>& devices, std::string* err, bool kernelTrace = false);
   bool initialized() const { return toolInitDone_; }
   const std::vector<AgentInfo>& agents() const { return agents_; }
   // Context for an agent index, or -1 if not configured.
@@ -69,6 +71,7 @@ class RocprofRuntime {
   bool preinitCalled_ = false;
   bool toolInitDone_ = false;
   std::vector<int> wantDevices_;
+  bool kernelTrace_ = false;
   std::vector<AgentInfo> agents_;
   std::map<int, std::unique_ptr<Ctx>> ctxs_;
   std::string err_;

@@ -25,6 +25,10 @@ void IpcMonitor::stop() {
   if (thread_.joinable()) thread_.join();
 }
 
+bool IpcMonitor::send(const std::string& type, const std::string& payload, const std::string& dest) {
+  return fabric_ && fabric_->syncSend(ipc::Message::fromString(type, payload), dest, 3, 1000);
+}
+
 bool IpcMonitor::processPending() {
   if (!fabric_ || !fabric_->recv()) return false;
   processMsg(fabric_->retrieve());
@@ -55,6 +59,13 @@ void IpcMonitor::processMsg(std::unique_ptr<ipc::Message> msg) {
     std::string err;
     if (metricsCb_ && Json::tryParse(std::string(msg->buf.begin(), msg->buf.end()), &j, &err))
       metricsCb_(j);
+  } else if (msg->typeIs(ipc::kMsgAgentContext) || msg->typeIs(ipc::kMsgKernelTraceResult)) {
+    Json j;
+    std::string err;
+    if (agents_ && Json::tryParse(std::string(msg->buf.begin(), msg->buf.end()), &j, &err)) {
+      if (msg->typeIs(ipc::kMsgAgentContext)) agents_->onContext(j, msg->src);
+      else agents_->onResult(j);
+    }
   } else {
     LOG(ERROR) << "IPC: unknown message type '" << msg->type() << "'";
   }

@@ -101,3 +101,39 @@ def test_agent_preinit_after_hip_init_fails_loudly(native_built):
     # it) the agent works; it must never silently run without counters.
     if not res["ok"]:
         assert "preinit" in res["err"] or "rocprofiler" in res["err"]
+
+
+def test_kernel_trace_in_process(native_built, tmp_path):
+    """rocprofiler-sdk kernel dispatch tracing owned by the agent: names from
+    code-object callbacks, per-kernel summary, Chrome trace, GPU tag-stack
+    slices."""
+    chrome = str(tmp_path / "kernels.json")
+    res = _run(f"""
+        from dynolog_amd import agent
+        agent.preinit(kernel_trace=True)
+        import json, torch
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        y = x @ x; torch.cuda.synchronize()            # warm up / load code objects
+        with agent.KernelTrace() as kt:
+            for _ in range(20):
+                y = x @ x
+                z = torch.nn.functional.silu(y)
+        s = kt.summary(top=5)
+        kt.write_chrome({chrome!r})
+        sl = kt.slices()
+        print("RESULT " + json.dumps(dict(summary=s, slices=sl)))
+    """)
+    s = res["summary"]
+    assert s["dispatches"] >= 40, s
+    assert s["dropped_records"] == 0
+    names = [k["name"] for k in s["top_kernels"]]
+    assert any(("Cijk" in n) or ("gemm" in n.lower()) for n in names), names
+    assert all(not n.startswith("kernel_") for n in names), names   # symbols resolved
+    assert 0 < s["gpu_busy_ms"] <= s["window_ms"] + 1.0
+    with open(chrome) as f:
+        tr = json.load(f)
+    evs = tr["traceEvents"]
+    assert len(evs) == s["dispatches"]
+    assert all(e["ph"] == "X" and e["dur"] >= 0 for e in evs)
+    gpu0 = res["slices"].get("gpu0", {})
+    assert gpu0 and sum(gpu0.values()) > 0
