@@ -48,6 +48,8 @@ def parse_args(argv=None):
     p.add_argument("--gather-mode", default="gather", choices=["gather", "allgather", "none"])
     p.add_argument("--counter-set", default="lite", help="lite (default) | full | core | comma list")
     p.add_argument("--no-agent", action="store_true", help="run the workload only")
+    p.add_argument("--kernel-trace-ready", action="store_true",
+                   help="also configure (idle) on-demand kernel tracing, to price its queue interception")
     p.add_argument("--skip-baseline", action="store_true")
     p.add_argument("--ab-rounds", type=int, default=4,
                    help="interleaved paused/sampling window pairs for the overhead estimate")
@@ -80,7 +82,8 @@ def main(argv=None) -> int:
         # is visible, as under torchrun on one node).
         visible = any(os.environ.get(v) for v in
                       ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"))
-        dagent.preinit(None if visible else [int(os.environ.get("LOCAL_RANK", "0"))])
+        dagent.preinit(None if visible else [int(os.environ.get("LOCAL_RANK", "0"))],
+                       kernel_trace=args.kernel_trace_ready)
 
     import torch
     from dynolog_amd.models.llama import CONFIGS, build_llama, lm_loss
@@ -214,6 +217,7 @@ def main(argv=None) -> int:
             "model": args.model, "global_batch": B * env.world, "seq_len": S,
             "parallelism": f"dp{env.world}", "sample_hz_target": args.sample_hz,
             "counter_set": args.counter_set, "gather": args.gather_mode, "pack_batch": args.pack_batch,
+            "kernel_trace_ready": args.kernel_trace_ready,
         },
         "samples_per_sec_per_gpu": round(value / env.world, 3),
         "samples_per_rank": per_rank,
