@@ -44,11 +44,13 @@ struct alignas(64) RingHeader {
   static_assert(std::atomic<uint64_t>::is_always_lock_free, "needs lock-free 64-bit atomics");
   static_assert(std::atomic<bool>::is_always_lock_free, "needs lock-free bool atomics");
 
+  // Each side's cursor shares a cache line only with that side's tx flag, so
+  // the producer's CAS + head store never bounce the consumer's line.
   alignas(64) std::atomic<uint64_t> head{0};  // producer cursor (bytes ever written)
+  std::atomic<bool> inWriteTx{false};
   alignas(64) std::atomic<uint64_t> tail{0};  // consumer cursor (bytes ever consumed)
-  alignas(64) std::atomic<bool> inWriteTx{false};
   std::atomic<bool> inReadTx{false};
-  uint64_t size = 0;  // data bytes (power of two)
+  alignas(64) uint64_t size = 0;  // data bytes (power of two); read-only after init
   uint64_t mask = 0;
   uint64_t magic = 0x52494e4748445231ull;  // "RINGHDR1"
   TExtra extra{};
@@ -120,15 +122,19 @@ class Producer {
   }
 
   // -EBUSY: another write transaction is open. -EAGAIN: ring is full.
+  // The consumer cursor is cached (tail only grows, so a stale copy merely
+  // under-reports free space) and re-read only when the ring looks full.
   [[nodiscard]] ssize_t startTx() {
     auto& h = rb_->header();
     bool expected = false;
     if (!h.inWriteTx.compare_exchange_strong(expected, true, std::memory_order_acq_rel)) return -EBUSY;
     head_ = h.head.load(std::memory_order_relaxed);
-    tail_ = h.tail.load(std::memory_order_acquire);
-    if (head_ - tail_ == h.size) {
-      h.inWriteTx.store(false, std::memory_order_release);
-      return -EAGAIN;
+    if (head_ - tail_ >= h.size) {
+      tail_ = h.tail.load(std::memory_order_acquire);
+      if (head_ - tail_ == h.size) {
+        h.inWriteTx.store(false, std::memory_order_release);
+        return -EAGAIN;
+      }
     }
     inTx_ = true;
     txSize_ = 0;
@@ -153,7 +159,10 @@ class Producer {
   // u32 length prefix + bytes (readable with Consumer::readSizedInTx)
   [[nodiscard]] ssize_t writeSizedInTx(const void* src, uint32_t n) noexcept {
     auto& h = rb_->header();
-    if (head_ + txSize_ + sizeof(n) + n - h.tail.load(std::memory_order_acquire) > h.size) return -ENOSPC;
+    if (head_ + txSize_ + sizeof(n) + n - tail_ > h.size) {
+      tail_ = h.tail.load(std::memory_order_acquire);
+      if (head_ + txSize_ + sizeof(n) + n - tail_ > h.size) return -ENOSPC;
+    }
     (void)writeInTx(sizeof(n), &n);
     return writeInTx(n, src);
   }
@@ -221,15 +230,19 @@ class Consumer {
     if (inTx_) (void)cancelTx();
   }
   // -EBUSY: another read transaction open. -EAGAIN: ring empty.
+  // The producer cursor is cached (head only grows) and re-read only when
+  // everything cached has been consumed.
   [[nodiscard]] ssize_t startTx() {
     auto& h = rb_->header();
     bool expected = false;
     if (!h.inReadTx.compare_exchange_strong(expected, true, std::memory_order_acq_rel)) return -EBUSY;
     tail_ = h.tail.load(std::memory_order_relaxed);
-    head_ = h.head.load(std::memory_order_acquire);
-    if (head_ == tail_) {
-      h.inReadTx.store(false, std::memory_order_release);
-      return -EAGAIN;
+    if (head_ <= tail_) {
+      head_ = h.head.load(std::memory_order_acquire);
+      if (head_ == tail_) {
+        h.inReadTx.store(false, std::memory_order_release);
+        return -EAGAIN;
+      }
     }
     inTx_ = true;
     txSize_ = 0;

@@ -6,6 +6,7 @@
 #include <thread>
 
 #include "metric_frame/MetricFrame.h"
+#include "metric_frame/ValueTimeSeries.h"
 #include "ring/RingBuffer.h"
 #include "tagstack/TagStack.h"
 #include "testing.h"
@@ -288,4 +289,24 @@ TEST(TagStack, IntervalSplitAndCombinator) {
   EXPECT_EQ(drain(comb, s, 100), 6u);
   EXPECT_EQ(s.stats().numOutOfOrder, 0u);
   ASSERT_EQ(out.size(), 3u);
+}
+
+TEST(MetricFrame, ValueTimeSeriesOrderedRangeAndWeightedMean) {
+  metric_frame::ValueTimeSeries<double> s;
+  s.add(100, 1.0);
+  s.add(300, 3.0);
+  s.add(200, 2.0);  // out of order: inserted in place
+  ASSERT_EQ(s.size(), 3u);
+  EXPECT_EQ(s[1].tstamp, 200);
+  EXPECT_NEAR(s.sum(), 6.0, 1e-12);
+  EXPECT_NEAR(s.at(250)->value, 2.0, 1e-12);
+  EXPECT_FALSE(s.at(50).has_value());
+  auto r = s.range(150, 300);
+  ASSERT_EQ(r.size(), 1u);
+  EXPECT_NEAR(r[0].value, 2.0, 1e-12);
+  // 1.0 for 100 ns then 2.0 for 100 ns
+  EXPECT_NEAR(s.timeWeightedMean(), 1.5, 1e-12);
+  s.trimBefore(200);
+  EXPECT_EQ(s.size(), 2u);
+  EXPECT_NEAR(s.last()->value, 3.0, 1e-12);
 }

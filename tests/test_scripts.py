@@ -40,3 +40,12 @@ def test_client_config_matches_cli():
     cfg = client.kineto_config("/tmp/t.json", iterations=3, start_iteration_roundup=10)
     assert cfg.endswith("PROFILE_START_ITERATION_ROUNDUP=10\nACTIVITIES_ITERATIONS=3")
     assert client.trace_files("/x/t.json", [5, 6]) == ["/x/t_5.json", "/x/t_6.json"]
+
+
+def test_linear_model_example_runs_on_cpu():
+    r = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "pytorch", "linear_model_example.py"),
+                        "--iterations", "3", "--batch", "8", "--dim", "16", "--device", "cpu",
+                        "--print-every", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("PID ")
+    assert "iter 3 loss" in r.stdout
