@@ -192,6 +192,7 @@ bool Daemon::start(std::string* err) {
   }
 
   if (FLAGS_enable_perf_monitor) startPerfMonitor(*this);
+  startSharedCounters(*this);  // no-op unless --shared_counters is set
   if (FLAGS_enable_gpu_counters) startGpuCounterMonitor(*this);
   return true;
 }

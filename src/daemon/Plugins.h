@@ -12,6 +12,8 @@ class RpcDispatcher;
 }
 
 void startPerfMonitor(Daemon& d);
+// Shared always-on counters published in shm (pmu/SharedCounters.h).
+void startSharedCounters(Daemon& d);
 void startGpuCounterMonitor(Daemon& d);
 void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d);
 void stopPlugins();
