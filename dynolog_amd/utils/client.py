@@ -71,3 +71,36 @@ def gputrace(log_file: str, job_id: int = 0, pids: Iterable[int] = (0,), process
 def trace_files(log_file: str, pids: Iterable[int]) -> list[str]:
     """Output files libkineto writes: log_file with '.json' -> '_<pid>.json'."""
     return [log_file.replace(".json", f"_{p}.json") for p in pids]
+
+
+def topology(**kw) -> dict:
+    """GPU <-> PCI BDF <-> xGMI hive <-> NUMA map and the GPU link matrix."""
+    return call({"fn": "getTopology"}, **kw)
+
+
+def gpu_agents(**kw) -> dict:
+    """In-process GPU agents registered with the daemon (IPC "gctx")."""
+    return call({"fn": "getGpuAgents"}, **kw)
+
+
+def gpu_kernel_trace(pids: Iterable[int] = (), duration_ms: int = 500, top: int = 20,
+                     chrome_dir: str = "", host: str = "localhost", port: int = DEFAULT_PORT) -> dict:
+    """On-demand GPU kernel trace through the agents of `pids` (all if empty)."""
+    req = {"fn": "gpuKernelTrace", "pids": list(pids), "duration_ms": duration_ms, "top": top}
+    if chrome_dir:
+        req["chrome_dir"] = chrome_dir
+    return call(req, host=host, port=port, timeout=duration_ms / 1000.0 + 20.0)
+
+
+def cpu_trace(pid: int = 0, duration_ms: int = 500, events: str = "task-clock,context-switches",
+              sample_period: int = 1_000_000, top: int = 20, ibs_period: int = 0,
+              host: str = "localhost", port: int = DEFAULT_PORT) -> dict:
+    """On-demand CPU trace: sampled counts per thread / tag stack (+ AMD IBS)."""
+    req = {"fn": "cpuTrace", "pid": pid, "duration_ms": duration_ms, "events": events,
+           "sample_period": sample_period, "top": top, "ibs_period": ibs_period}
+    return call(req, host=host, port=port, timeout=duration_ms / 1000.0 + 15.0)
+
+
+def metrics(collector: str = "kernel", last: int = 1, **kw) -> dict:
+    """Recent records of a collector from the daemon's metric store."""
+    return call({"fn": "getMetrics", "collector": collector, "last": last}, **kw)

@@ -29,11 +29,12 @@ SLOT_DTYPE = np.dtype([
     ("seq", "<u8"), ("host_ts_ns", "<u8"), ("gpu_pack_ticks", "<u8"),
     ("rank", "<u4"), ("flags", "<u4"),
     ("delta", "<u8", (MAX_COUNTERS,)), ("derived", "<f4", (MAX_DERIVED,)),
-    ("sample_latency_ns", "<u4"), ("n_records", "<u4"), ("reserved", "<u4", (6,)),
+    ("sample_latency_ns", "<u4"), ("n_records", "<u4"), ("phase", "<u4"), ("reserved", "<u4", (5,)),
 ])
 assert SLOT_DTYPE.itemsize == SLOT_BYTES
 
-STAGE_META_DTYPE = np.dtype([("host_ts_ns", "<u8"), ("latency_ns", "<u4"), ("n_records", "<u4")])
+STAGE_META_DTYPE = np.dtype([("host_ts_ns", "<u8"), ("latency_ns", "<u4"), ("n_records", "<u4"),
+                             ("phase", "<u4"), ("pad", "<u4")])
 
 GATHER_HEADER_DTYPE = np.dtype([
     ("first_seq", "<u8"), ("count", "<u4"), ("rank", "<u4"), ("dropped", "<u8"),

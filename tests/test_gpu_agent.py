@@ -137,3 +137,40 @@ def test_kernel_trace_in_process(native_built, tmp_path):
     assert all(e["ph"] == "X" and e["dur"] >= 0 for e in evs)
     gpu0 = res["slices"].get("gpu0", {})
     assert gpu0 and sum(gpu0.values()) > 0
+
+
+def test_phase_markers_attribute_samples(native_built):
+    """GPU-stream phase markers: samples taken while the GPU runs the GEMM
+    phase show MFMA work, samples in the copy phase show HBM traffic."""
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit()
+        import json, time, torch
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), log_interval_ms=200)
+        x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+        big = torch.empty(1 << 30, device="cuda", dtype=torch.uint8)
+        dst = torch.empty_like(big)
+        end = time.time() + 3.0
+        while time.time() < end:
+            with a.phase("step"):
+                with a.phase("gemm"):
+                    for _ in range(8):
+                        y = x @ x
+                with a.phase("copy"):
+                    for _ in range(40):
+                        dst.copy_(big)
+            torch.cuda.synchronize()
+            a.step()
+        a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+        st = a.phase_stats()
+        recs = [r for r in a.memory_records() if "phase" in r]
+        a.stop()
+        print("RESULT " + json.dumps(dict(stats=st, phase_records=recs[-4:])))
+    """)
+    per = res["stats"]["0"]
+    gemm, copy = per["step/gemm"], per["step/copy"]
+    assert gemm["samples"] > 200 and copy["samples"] > 200, per.keys()
+    assert gemm["mfma_util"] > 5 * max(copy["mfma_util"], 0.1), (gemm, copy)
+    hbm = lambda p: p["hbm_read_gbps"] + p["hbm_write_gbps"]
+    assert hbm(copy) > 2 * hbm(gemm), (gemm, copy)
+    assert res["phase_records"], "per-phase interval records missing"

@@ -59,4 +59,4 @@ def test_host_pack_matches_reference(native_built, with_prev):
 
 def test_slot_layout_is_256_bytes():
     assert S.SLOT_DTYPE.itemsize == S.SLOT_BYTES == 256
-    assert S.STAGE_META_DTYPE.itemsize == 16
+    assert S.STAGE_META_DTYPE.itemsize == 24
