@@ -48,6 +48,8 @@ def parse_args(argv=None):
     p.add_argument("--gather-mode", default="gather", choices=["gather", "allgather", "none"])
     p.add_argument("--counter-set", default="lite", help="lite (default) | full | core | comma list")
     p.add_argument("--no-agent", action="store_true", help="run the workload only")
+    p.add_argument("--phases", action="store_true",
+                   help="mark forward/backward/optimizer on the GPU stream and report per-phase metrics")
     p.add_argument("--kernel-trace-ready", action="store_true",
                    help="also configure (idle) on-demand kernel tracing, to price its queue interception")
     p.add_argument("--skip-baseline", action="store_true")
@@ -112,13 +114,21 @@ def main(argv=None) -> int:
                                    sinks=("json", "memory"))
 
     last_loss = [0.0]
+    import contextlib
+    use_phases = ag is not None and args.phases
+
+    def ph(name):
+        return ag.phase(name) if use_phases else contextlib.nullcontext()
 
     def train_step():
-        logits = model(inputs)
-        loss = lm_loss(logits, targets)
-        loss.backward()
-        opt.step()
-        opt.zero_grad(set_to_none=True)
+        with ph("forward"):
+            logits = model(inputs)
+            loss = lm_loss(logits, targets)
+        with ph("backward"):
+            loss.backward()
+        with ph("optimizer"):
+            opt.step()
+            opt.zero_grad(set_to_none=True)
         if ag is not None:
             ag.step()  # rank-0 gather of new counter slots, on the current stream
         last_loss[0] = loss
@@ -217,7 +227,7 @@ def main(argv=None) -> int:
             "model": args.model, "global_batch": B * env.world, "seq_len": S,
             "parallelism": f"dp{env.world}", "sample_hz_target": args.sample_hz,
             "counter_set": args.counter_set, "gather": args.gather_mode, "pack_batch": args.pack_batch,
-            "kernel_trace_ready": args.kernel_trace_ready,
+            "kernel_trace_ready": args.kernel_trace_ready, "phases": args.phases,
         },
         "samples_per_sec_per_gpu": round(value / env.world, 3),
         "samples_per_rank": per_rank,
@@ -235,6 +245,13 @@ def main(argv=None) -> int:
                         ("samples_taken", "samples_failed", "sample_latency_us_avg",
                          "sample_latency_us_max", "late_ticks", "gathers", "raw_instances",
                          "last_error")}
+    if use_phases and env.rank == 0:
+        keep = ("samples", "gpu_busy_pct", "mfma_util", "mfma_bf16_tflops", "hbm_read_gbps",
+                "hbm_write_gbps", "lds_bank_conflict_rate", "occupancy_pct")
+        out["phases"] = {rank: {name: {k: round(v, 3) if isinstance(v, float) else v
+                                       for k, v in p.items() if k in keep}
+                                for name, p in per.items()}
+                         for rank, per in ag.phase_stats().items()}
     if env.rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
