@@ -85,6 +85,26 @@ std::shared_ptr<RpcDispatcher> makeDispatcher(std::shared_ptr<ServiceHandler> h)
   d->add("getKinetoProcesses",
          [h](const Json&) -> std::optional<Json> { return h->getKinetoProcesses(); });
   d->add("listCollectors", [h](const Json&) -> std::optional<Json> { return h->listCollectors(); });
+  // {"fn":"getMetricStats","collector":"gpu","key":"gpu_power_draw",
+  //  "window_s":60,"filter_key":"device","filter_value":0}
+  d->add("getMetricStats", [h](const Json& req) -> std::optional<Json> {
+    Json r = Json::object();
+    if (!h->store() || !req.contains("key") || !req.at("key").isString()) {
+      r["status"] = "failed";
+      return r;
+    }
+    const std::string c = req.contains("collector") && req.at("collector").isString()
+                              ? req.at("collector").asString()
+                              : "kernel";
+    const int64_t windowMs = req.contains("window_s") && req.at("window_s").isNumber()
+                                 ? static_cast<int64_t>(req.at("window_s").asDouble() * 1000.0)
+                                 : 0;
+    const std::string fk = req.contains("filter_key") && req.at("filter_key").isString()
+                               ? req.at("filter_key").asString()
+                               : "";
+    return h->store()->stats(c, req.at("key").asString(), windowMs, fk,
+                             req.contains("filter_value") ? req.at("filter_value") : Json());
+  });
   d->add("getMetrics", [h](const Json& req) -> std::optional<Json> {
     try {
       std::string c = req.contains("collector") ? req.at("collector").asString() : "kernel";

@@ -35,6 +35,7 @@ class ServiceHandler {
   virtual Json listCollectors();
 
   void setMetricStore(std::shared_ptr<MetricStore> s) { store_ = std::move(s); }
+  const std::shared_ptr<MetricStore>& store() const { return store_; }
   void setConfigManager(tracing::KinetoConfigManager* m) { mgr_ = m; }
 
  protected:

@@ -2,9 +2,10 @@
 // dashboards: bounded history of finalized records per collector.
 // The reference keeps no queryable history at all (its metric_frame library
 // is never wired to main(), SURVEY.md §0 "Lib"); here every collector's
-// records land in a MetricStore through StoreLogger, and numeric keys are
-// also appended to per-collector MetricFrames (src/metric_frame) for
-// rate/avg/percentile queries.
+// records land in a MetricStore through StoreLogger, and stats() runs the
+// metric_frame series statistics (avg/min/max/percentiles/rate,
+// src/metric_frame/MetricFrame.h MetricSeries) over a key in a time window —
+// the daemon's getMetricStats RPC.
 #pragma once
 
 #include <deque>
@@ -26,6 +27,12 @@ class MetricStore {
   Json last(const std::string& collector, int n) const;
   std::vector<std::string> collectors() const;
   size_t size(const std::string& collector) const;
+  // Statistics of numeric `key` over records of the last `windowMs` (0 = all
+  // retained), optionally only records whose `filterKey` equals
+  // `filterValue` (e.g. device=3). Keys: count, avg, min, max, p50, p90,
+  // p99, last, first_ts_ms, last_ts_ms, rate_per_s (of the value's change).
+  Json stats(const std::string& collector, const std::string& key, int64_t windowMs,
+             const std::string& filterKey = "", const Json& filterValue = Json()) const;
 
  private:
   size_t cap_;
