@@ -68,6 +68,11 @@ AgentConfig AgentConfig::fromJson(const Json& j) {
   if (j.contains("log_file")) c.logFile = j.at("log_file").asString();
   if (j.contains("daemon_endpoint")) c.daemonEndpoint = j.at("daemon_endpoint").asString();
   if (j.contains("pin_threads")) c.pinThreads = j.at("pin_threads").asBool();
+  if (j.contains("fault_inject")) {
+    // "gather_error@N": behave as if RCCL reported an async error at step N
+    const std::string f = j.at("fault_inject").asString();
+    if (f.rfind("gather_error@", 0) == 0) c.faultGatherAtStep = std::strtoull(f.c_str() + 13, nullptr, 10);
+  }
   if (j.contains("sinks")) {
     c.sinks.clear();
     for (const auto& s : j.at("sinks").asArray()) c.sinks.push_back(s.asString());
@@ -455,6 +460,25 @@ bool Agent::step(hipStream_t stream, std::string* err) {
   steps_++;
   if (paused_) return true;  // every rank pauses at the same program point
   if (cfg_.gatherMode == "none" && cfg_.world > 1) return true;
+  if (gatherFailed_) return true;  // degraded: keep sampling locally, never block training
+  // Failure detection on the metrics path: an RCCL async error (peer lost,
+  // network fault) or an injected fault disables gathers for good instead of
+  // hanging or crashing the trainer. Same program point on every rank.
+  ncclResult_t async = ncclSuccess;
+  if (comm_) ncclCommGetAsyncError(comm_, &async);
+  const bool injected = cfg_.faultGatherAtStep > 0 && steps_ >= cfg_.faultGatherAtStep;
+  if ((async != ncclSuccess && async != ncclInProgress) || injected) {
+    gatherFailed_ = true;
+    lastError_ = injected ? "injected gather fault at step " + std::to_string(steps_.load())
+                          : std::string("RCCL async error: ") + ncclGetErrorString(async);
+    LOG(ERROR) << "GPU agent rank " << cfg_.rank << ": " << lastError_
+               << "; counter gathers disabled, sampling continues locally";
+    if (comm_ && !injected) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+    return true;
+  }
   hipEvent_t pack = nullptr;
   {
     std::lock_guard<std::mutex> pg(packMu_);
@@ -764,6 +788,8 @@ Json Agent::stats() const {
   j["sample_latency_us_max"] = latencyMaxNs_.load() * 1e-3;
   j["raw_instances"] = static_cast<unsigned long long>(R_);
   j["counter_set"] = cfg_.counterSet;
+  j["gather_failed"] = gatherFailed_.load();
+  j["steps"] = static_cast<unsigned long long>(steps_.load());
   j["sampler_affinity"] = pinnedCpus_;
   {
     Json names = Json::array();

@@ -59,6 +59,7 @@ struct AgentConfig {
   bool pinThreads = true;            // sampler/consumer on the GPU's NUMA-local CPUs
   bool daemonControl = false;        // register with the daemon, serve kernel-trace requests
                                      // (default: on when the "daemon" sink is used)
+  uint64_t faultGatherAtStep = 0;    // fault injection ("gather_error@N"), 0 = off
 
   static AgentConfig fromJson(const Json& j);
 };
@@ -133,6 +134,7 @@ class Agent {
   std::atomic<bool> stopFlag_{false};
   std::atomic<bool> paused_{false};
   std::atomic<bool> resetPrev_{false};
+  std::atomic<bool> gatherFailed_{false};
   std::atomic<uint64_t> flushReq_{0}, flushAck_{0};
   std::atomic<uint64_t> periodNs_{1000000};
   std::thread samplerThread_, consumerThread_, ctlThread_;

@@ -174,3 +174,30 @@ def test_phase_markers_attribute_samples(native_built):
     hbm = lambda p: p["hbm_read_gbps"] + p["hbm_write_gbps"]
     assert hbm(copy) > 2 * hbm(gemm), (gemm, copy)
     assert res["phase_records"], "per-phase interval records missing"
+
+
+def test_gather_fault_degrades_without_blocking_training(native_built):
+    """An RCCL async error on the metrics path (injected here) disables the
+    gathers at the same program point; training steps keep running and the
+    error is reported in stats."""
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit()
+        import json, torch
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",),
+                                 fault_inject="gather_error@4")
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        for _ in range(8):
+            for _ in range(20):
+                y = x @ x
+            a.step()
+        torch.cuda.synchronize(); a.flush()
+        st = a.stats()
+        a.stop()
+        print("RESULT " + json.dumps(st))
+    """)
+    assert res["gather_failed"] is True
+    assert res["steps"] == 8
+    assert res["gathers"] == 3, res          # steps 1..3 gathered, 4.. skipped
+    assert "injected gather fault" in res["last_error"]
+    assert res["samples_taken"] > 0 and res["samples_failed"] == 0
