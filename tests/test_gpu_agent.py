@@ -201,3 +201,12 @@ def test_gather_fault_degrades_without_blocking_training(native_built):
     assert res["gathers"] == 3, res          # steps 1..3 gathered, 4.. skipped
     assert "injected gather fault" in res["last_error"]
     assert res["samples_taken"] > 0 and res["samples_failed"] == 0
+
+
+def test_train_with_agent_example_runs(native_built):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "examples", "train_with_agent.py"),
+                        "--model", "tiny", "--steps", "30", "--seq-len", "128"],
+                       cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads(r.stdout[r.stdout.index("{"):])
+    assert set(out["phases"]["0"]) >= {"forward", "backward", "optimizer"}
