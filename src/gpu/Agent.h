@@ -177,6 +177,8 @@ class Agent {
   hipEvent_t packEvents_[8] = {};
   int packEventNext_ = 0;
   hipEvent_t lastPack_ = nullptr;
+  uint64_t lastPackHead_ = 0;   // ring head once lastPack_ completes (packMu_)
+  uint64_t gatheredHost_ = 0;   // slots already handed to a gather (stepMu_)
 
   ncclComm_t comm_ = nullptr;
   std::mutex stepMu_;
