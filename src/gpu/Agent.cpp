@@ -68,6 +68,8 @@ AgentConfig AgentConfig::fromJson(const Json& j) {
   if (j.contains("log_file")) c.logFile = j.at("log_file").asString();
   if (j.contains("daemon_endpoint")) c.daemonEndpoint = j.at("daemon_endpoint").asString();
   if (j.contains("pin_threads")) c.pinThreads = j.at("pin_threads").asBool();
+  if (j.contains("slot_ring")) c.slotRing = j.at("slot_ring").asString();
+  gi("slot_ring_bytes", c.slotRingBytes);
   if (j.contains("fault_inject")) {
     // "gather_error@N": behave as if RCCL reported an async error at step N
     const std::string f = j.at("fault_inject").asString();
@@ -272,6 +274,17 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   }
 
   agg_.assign(static_cast<size_t>(cfg_.world), RankAggregate{});
+  if (root && !cfg_.slotRing.empty()) {
+    // Host ring of the device ring: every slot rank 0
+    // receives is re-published, all ranks interleaved, in a lock-free shm ring
+    // that any local process can consume at full rate.
+    try {
+      slotRing_ = ring::ShmRing<>::create(cfg_.slotRing, std::max<uint64_t>(nextPow2(cfg_.slotRingBytes), 1 << 16));
+      slotProd_ = std::make_unique<ring::Producer<>>(slotRing_->ring());
+    } catch (const std::exception& e) {
+      LOG(WARNING) << "GPU agent: slot ring '" << cfg_.slotRing << "' unavailable: " << e.what();
+    }
+  }
   memStore_ = std::make_shared<MemoryLogger::Store>();
   memStore_->capacity = cfg_.memoryRecords;
   logger_ = makeLogger();
@@ -590,6 +603,11 @@ void Agent::consumerLoop() {
           }
           a.ts.push_back(s.host_ts_ns);
           a.last = s;
+          if (slotProd_ && slotProd_->write(s) < 0) {
+            // full: drop the oldest slot (the reader fell behind) and retry
+            if (slotProd_->dropN(sizeof(DynoSlot)) > 0) ++slotRingDropped_;
+            (void)slotProd_->write(s);
+          }
         }
         // keep the windowed-count history bounded (~10 minutes at 1 kHz)
         if (a.ts.size() > (1u << 20)) a.ts.erase(a.ts.begin(), a.ts.begin() + (1 << 19));
@@ -774,6 +792,8 @@ void Agent::stop() {
   if (consumerThread_.joinable()) consumerThread_.join();
   if (ctlThread_.joinable()) ctlThread_.join();
   ctl_.reset();
+  slotProd_.reset();
+  slotRing_.reset();  // unlinks the shm segments (the Agent itself is never destroyed)
   sampler_->stop();
   hipSetDevice(cfg_.device);
   hipDeviceSynchronize();
@@ -804,6 +824,10 @@ Json Agent::stats() const {
   j["raw_instances"] = static_cast<unsigned long long>(R_);
   j["counter_set"] = cfg_.counterSet;
   j["gather_failed"] = gatherFailed_.load();
+  if (slotRing_) {
+    j["slot_ring"] = cfg_.slotRing;
+    j["slot_ring_dropped"] = static_cast<unsigned long long>(slotRingDropped_);
+  }
   j["steps"] = static_cast<unsigned long long>(steps_.load());
   j["sampler_affinity"] = pinnedCpus_;
   {

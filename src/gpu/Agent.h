@@ -30,6 +30,7 @@
 #include "common/Json.h"
 #include "gpu/RocprofSampler.h"
 #include "gpu/SlotFormat.h"
+#include "ring/RingBuffer.h"
 #include "sinks/Logger.h"
 
 typedef struct ncclComm* ncclComm_t;
@@ -60,6 +61,8 @@ struct AgentConfig {
   bool daemonControl = false;        // register with the daemon, serve kernel-trace requests
                                      // (default: on when the "daemon" sink is used)
   uint64_t faultGatherAtStep = 0;    // fault injection ("gather_error@N"), 0 = off
+  std::string slotRing;              // rank 0: publish every received slot into this shm ring
+  uint64_t slotRingBytes = 64ull << 20;  // (256k slots = ~4 min of 1 kHz x 1 GPU)
 
   static AgentConfig fromJson(const Json& j);
 };
@@ -201,6 +204,9 @@ class Agent {
   uint64_t startNs_ = 0;
   std::string pinnedCpus_;
   uint32_t* hPhase_ = nullptr;                  // GPU-written current phase (coherent pinned)
+  std::unique_ptr<ring::ShmRing<>> slotRing_;   // raw slot export (consumer thread)
+  std::unique_ptr<ring::Producer<>> slotProd_;
+  uint64_t slotRingDropped_ = 0;
   std::map<uint32_t, std::string> phaseNames_;  // guarded by aggMu_
 };
 

@@ -3,6 +3,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <cstddef>
 #include <thread>
 
 #include "metric_frame/MetricFrame.h"
@@ -309,4 +310,16 @@ TEST(MetricFrame, ValueTimeSeriesOrderedRangeAndWeightedMean) {
   s.trimBefore(200);
   EXPECT_EQ(s.size(), 2u);
   EXPECT_NEAR(s.last()->value, 3.0, 1e-12);
+}
+
+TEST(RingBuffer, HeaderLayoutPinnedForPythonReaders) {
+  // dynolog_amd/utils/slot_ring.py reads these offsets directly from /dev/shm
+  using H = ring::RingHeader<>;
+  EXPECT_EQ(offsetof(H, head), 0u);
+  EXPECT_EQ(offsetof(H, tail), 64u);
+  EXPECT_EQ(offsetof(H, size), 128u);
+  EXPECT_EQ(offsetof(H, mask), 136u);
+  EXPECT_EQ(offsetof(H, magic), 144u);
+  H h;
+  EXPECT_EQ(h.magic, 0x52494e4748445231ull);
 }
