@@ -157,7 +157,7 @@ void startGpuCounterMonitor(Daemon& d) {
 }
 
 void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d) {
-  disp.add("getPmuMetrics", [](const Json&) -> std::optional<Json> {
+  disp.add("getPmuMetrics", [](const Json& req) -> std::optional<Json> {
     Json j = Json::object();
     auto ms = pmu::getDefaultMetrics();
     Json arr = Json::array();
@@ -171,8 +171,20 @@ void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d) {
     auto mgr = pmu::getDefaultPmuDeviceManager();
     j["arch"] = pmu::cpuArchName(mgr->arch());
     Json pmus = Json::array();
-    for (const auto& [n, dev] : mgr->devices()) pmus.push_back(n);
+    Json nEvents = Json::object();
+    for (const auto& [n, dev] : mgr->devices()) {
+      pmus.push_back(n);
+      nEvents[n] = static_cast<int64_t>(dev.aliases.size());
+    }
     j["pmus"] = pmus;
+    j["pmu_event_counts"] = nEvents;
+    if (req.contains("pmu") && req.at("pmu").isString()) {
+      Json evs = Json::object();
+      if (const auto* dev = mgr->find(req.at("pmu").asString())) {
+        for (const auto& [name, fields] : dev->aliases) evs[name] = fields;
+      }
+      j["events"] = evs;
+    }
     j["active"] = gPerf ? Json(gPerf->activeMetrics()) : Json::array();
     return j;
   });
