@@ -11,6 +11,7 @@
 
 #include "common/Logging.h"
 #include "common/System.h"
+#include "mon/IbsProfile.h"
 #include "mon/MonData.h"
 #include "mon/TraceCollector.h"
 #include "pmu/PerfMonitor.h"
@@ -36,28 +37,10 @@ Json runIbs(int pid, const CpuSet& cpus, uint64_t period, int durationMs, mon::T
   auto mgr = pmu::getDefaultPmuDeviceManager();
   pmu::IbsOpSampler ibs(*mgr, cpus, period);
   if (!ibs.open(err)) return Json();
-  struct Agg {
-    uint64_t ops = 0, loads = 0, stores = 0, dcMiss = 0, mispred = 0, missLatSum = 0;
-  };
-  std::map<std::string, Agg> byModule;
-  Agg all;
   std::optional<mon::ModuleInfo> mods;
   if (pid > 0) mods = mon::ModuleInfo::load(pid);
-  auto fn = [&](const pmu::IbsOpSample& s) {
-    if (pid > 0 && s.pid != static_cast<uint32_t>(pid)) return;
-    std::string m = "[unknown]";
-    if (mods) {
-      if (const auto* mod = mods->find(s.rip)) m = mod->path;
-    }
-    for (Agg* a : {&byModule[m], &all}) {
-      a->ops++;
-      a->loads += s.load;
-      a->stores += s.store;
-      a->dcMiss += s.dcMiss;
-      a->mispred += s.branchMispredicted;
-      if (s.dcMiss) a->missLatSum += s.dcMissLatency;
-    }
-  };
+  mon::IbsProfile prof(pid, std::move(mods));
+  auto fn = [&](const pmu::IbsOpSample& s) { prof.add(s); };
   ibs.enable();
   const auto end = std::chrono::steady_clock::now() + std::chrono::milliseconds(durationMs);
   while (std::chrono::steady_clock::now() < end) {
@@ -67,21 +50,7 @@ Json runIbs(int pid, const CpuSet& cpus, uint64_t period, int durationMs, mon::T
   }
   ibs.disable();
   ibs.poll(fn);
-  auto render = [](const Agg& a) {
-    Json j = Json::object();
-    j["ops"] = static_cast<unsigned long long>(a.ops);
-    j["loads"] = static_cast<unsigned long long>(a.loads);
-    j["stores"] = static_cast<unsigned long long>(a.stores);
-    j["dc_miss_rate"] = a.loads + a.stores ? double(a.dcMiss) / double(a.loads + a.stores) : 0.0;
-    j["avg_dc_miss_latency_cycles"] = a.dcMiss ? double(a.missLatSum) / double(a.dcMiss) : 0.0;
-    j["branch_mispredicts"] = static_cast<unsigned long long>(a.mispred);
-    return j;
-  };
-  Json out = Json::object();
-  out["total"] = render(all);
-  Json mj = Json::object();
-  for (const auto& [m, a] : byModule) mj[m] = render(a);
-  out["by_module"] = mj;
+  Json out = prof.toJson();
   out["lost"] = static_cast<unsigned long long>(ibs.lost());
   return out;
 }
