@@ -44,17 +44,6 @@ void deviceCountingCb(rocprofiler_context_id_t context_id, rocprofiler_agent_id_
 
 }  // namespace
 
-const std::vector<std::string>& defaultCounterNames() {
-  static const std::vector<std::string> names = {
-      "SQ_WAVES",          "SQ_BUSY_CYCLES",       "SQ_WAVE_CYCLES",
-      "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_LDS",
-      "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",  "TCC_EA0_RDREQ",
-      "TCC_EA0_WRREQ",     "TCC_EA0_WRREQ_64B",    "TCC_EA0_RDREQ_32B",
-      "GRBM_GUI_ACTIVE",   "GRBM_COUNT"};
-  static_assert(DC_NUM_COUNTERS == 14, "keep names in sync with DynoCounter");
-  return names;
-}
-
 std::vector<std::string> counterNamesForSet(const std::string& set, std::string* err) {
   std::vector<std::string> names = defaultCounterNames();
   auto disable = [&](std::initializer_list<int> slots) {
@@ -87,15 +76,6 @@ std::vector<std::string> counterNamesForSet(const std::string& set, std::string*
     start = comma + 1;
   }
   return out;
-}
-
-const std::vector<std::string>& derivedMetricNames() {
-  static const std::vector<std::string> names = {
-      "gpu_busy_pct",  "mfma_util",     "mfma_bf16_tflops",  "hbm_read_gbps",
-      "hbm_write_gbps", "lds_bank_conflict_rate", "occupancy_pct", "waves_per_us",
-      "sq_busy_pct",   "lds_insts_per_us", "sclk_mhz",         "sample_dt_us"};
-  static_assert(DD_NUM_DERIVED == 12, "keep names in sync with DynoDerived");
-  return names;
 }
 
 DynoAgentConsts makeAgentConsts(const AgentInfo& a) {

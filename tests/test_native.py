@@ -7,7 +7,7 @@ import pytest
 
 SUITES = ["Json", "Flags", "System", "KernelCollector", "Sinks", "SmiMonitor", "Rpc",
           "KinetoConfigManager", "IpcFabric", "IpcMonitor", "Pmu", "MetricFrame",
-          "RingBuffer", "TagStack", "PerfSampling", "Mon"]
+          "RingBuffer", "TagStack", "PerfSampling", "Mon", "GpuHost"]
 
 
 @pytest.mark.parametrize("suite", SUITES)
