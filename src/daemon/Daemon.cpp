@@ -1,6 +1,8 @@
 #include "daemon/Daemon.h"
 
 #include <sys/prctl.h>
+#include <sys/resource.h>
+#include <time.h>
 
 #include <algorithm>
 
@@ -9,6 +11,7 @@
 #include "common/Flags.h"
 #include "common/Logging.h"
 #include "common/Sync.h"
+#include "common/System.h"
 #include "daemon/Plugins.h"
 #include "rpc/RpcServer.h"
 #include "rpc/ServiceHandler.h"
@@ -67,16 +70,38 @@ bool Daemon::sleepFor(int ms) {
   return !stop_;
 }
 
+namespace {
+uint64_t threadCpuNs() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return static_cast<uint64_t>(ts.tv_sec) * 1000000000ull + static_cast<uint64_t>(ts.tv_nsec);
+}
+}  // namespace
+
 void Daemon::addLoop(const std::string& name, int intervalMs, std::function<void()> fn) {
-  loops_.emplace_back([this, name, intervalMs, fn]() {
+  LoopStats* st;
+  {
+    std::lock_guard<std::mutex> lk(loopStatsMu_);
+    st = &loopStats_.emplace_back();
+    st->name = name;
+    st->intervalMs = intervalMs;
+  }
+  loops_.emplace_back([this, name, intervalMs, fn, st]() {
     prctl(PR_SET_NAME, name.substr(0, 15).c_str(), 0, 0, 0);
     auto next = std::chrono::steady_clock::now();
     while (!stop_) {
+      const uint64_t w0 = nowNsMonotonic(), c0 = threadCpuNs();
       try {
         fn();
       } catch (const std::exception& e) {
         LOG(ERROR) << name << " loop: " << e.what();
+        st->errors++;
       }
+      const uint64_t wall = nowNsMonotonic() - w0;
+      st->ticks++;
+      st->wallNsSum += wall;
+      st->cpuNsSum += threadCpuNs() - c0;
+      if (wall > st->wallNsMax.load()) st->wallNsMax = wall;
       next += std::chrono::milliseconds(intervalMs);
       auto now = std::chrono::steady_clock::now();
       if (next < now) next = now;
@@ -87,12 +112,46 @@ void Daemon::addLoop(const std::string& name, int intervalMs, std::function<void
   });
 }
 
+Json Daemon::statsJson() const {
+  Json j = Json::object();
+  const uint64_t now = nowNsMonotonic();
+  const double up = (now - startNs_) * 1e-9;
+  j["uptime_s"] = up;
+  rusage ru{};
+  getrusage(RUSAGE_SELF, &ru);
+  const double cpu = ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6 + ru.ru_stime.tv_sec +
+                     ru.ru_stime.tv_usec * 1e-6;
+  j["cpu_s"] = cpu;
+  j["cpu_pct"] = up > 0 ? 100.0 * cpu / up : 0.0;  // of one core, since start
+  j["max_rss_kb"] = static_cast<int64_t>(ru.ru_maxrss);
+  Json loops = Json::object();
+  std::lock_guard<std::mutex> lk(loopStatsMu_);
+  for (const auto& st : loopStats_) {
+    Json l = Json::object();
+    const uint64_t n = st.ticks.load();
+    l["interval_ms"] = st.intervalMs;
+    l["ticks"] = static_cast<unsigned long long>(n);
+    l["errors"] = static_cast<unsigned long long>(st.errors.load());
+    l["avg_tick_us"] = n ? st.wallNsSum.load() / double(n) * 1e-3 : 0.0;
+    l["max_tick_us"] = st.wallNsMax.load() * 1e-3;
+    l["avg_tick_cpu_us"] = n ? st.cpuNsSum.load() / double(n) * 1e-3 : 0.0;
+    // CPU share of one core this loop costs at its configured interval
+    l["cpu_pct_at_interval"] =
+        n && st.intervalMs > 0 ? st.cpuNsSum.load() / double(n) / (st.intervalMs * 1e4) : 0.0;
+    loops[st.name] = l;
+  }
+  j["loops"] = loops;
+  return j;
+}
+
 bool Daemon::start(std::string* err) {
+  startNs_ = nowNsMonotonic();
   handler_ = std::make_shared<rpc::ServiceHandler>();
   handler_->setMetricStore(store_);
   auto dispatcher = rpc::makeDispatcher(handler_);
   registerPluginRpcs(*dispatcher, *this);
   gpuAgents_ = std::make_shared<tracing::GpuAgentRegistry>();
+  dispatcher->add("getDaemonStats", [this](const Json&) -> std::optional<Json> { return statsJson(); });
   dispatcher->add("getGpuAgents", [this](const Json&) -> std::optional<Json> { return gpuAgents_->listJson(); });
   // On-demand GPU kernel trace through the in-process agents (IPC "gktr").
   dispatcher->add("gpuKernelTrace", [this](const Json& req) -> std::optional<Json> {
