@@ -53,7 +53,7 @@ def parse_args(argv=None):
     p.add_argument("--kernel-trace-ready", action="store_true",
                    help="also configure (idle) on-demand kernel tracing, to price its queue interception")
     p.add_argument("--skip-baseline", action="store_true")
-    p.add_argument("--ab-rounds", type=int, default=4,
+    p.add_argument("--ab-rounds", type=int, default=6,
                    help="interleaved paused/sampling window pairs for the overhead estimate")
     p.add_argument("--ab-steps", type=int, default=5, help="steps per A/B window")
     p.add_argument("--log-file", default="", help="agent log destination (default stderr)")
