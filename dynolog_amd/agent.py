@@ -170,7 +170,7 @@ class GpuAgent:
               log_interval_ms: int = 1000, sinks: Sequence[str] = ("json",),
               log_file: str = "", uid: Optional[bytes] = None, process_group=None,
               daemon_endpoint: str = "dynolog", fault_inject: str = "",
-              slot_ring: str = "") -> "GpuAgent":
+              slot_ring: str = "", stages: int = 64) -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
@@ -188,6 +188,7 @@ class GpuAgent:
             dist.broadcast_object_list(obj, src=0, group=process_group)
             uid = obj[0]
         cfg = dict(device=device, rank=rank, world=world, sample_hz=sample_hz, batch=batch,
+                   stages=stages,
                    ring_slots=ring_slots, gather_cap_slots=gather_cap_slots,
                    gather_mode=gather_mode, counter_set=counter_set, log_interval_ms=log_interval_ms,
                    sinks=list(sinks), log_file=log_file, daemon_endpoint=daemon_endpoint)

@@ -66,6 +66,7 @@ AgentConfig AgentConfig::fromJson(const Json& j) {
   gi("world", c.world);
   gi("sample_hz", c.sampleHz);
   gi("batch", c.batch);
+  gi("stages", c.stages);
   gi("ring_slots", c.ringSlots);
   gi("gather_cap_slots", c.gatherCapSlots);
   gi("log_interval_ms", c.logIntervalMs);
@@ -235,12 +236,22 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     HIP_OK(hipMemsetAsync(c, 0, R_ * sizeof(double), packStream_), "memset carry");
   }
   const size_t stageBytes = B * sizeof(DynoStageMeta) + B * R_ * sizeof(double);
-  for (int i = 0; i < kStage; ++i) {
-    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hStage_[i]), stageBytes, hipHostMallocDefault),
-           "hipHostMalloc stage");
-    HIP_OK(hipEventCreateWithFlags(&stageDone_[i], hipEventDisableTiming), "event");
+  nStage_ = std::clamp(cfg_.stages, 2, kMaxStage);
+  for (int i = 0; i < nStage_; ++i) {
+    if (!hStage_[i]) {  // kept across stop()/start() of the process-wide agent
+      HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hStage_[i]), stageBytes, hipHostMallocDefault),
+             "hipHostMalloc stage");
+      HIP_OK(hipEventCreateWithFlags(&stageDone_[i], hipEventDisableTiming), "event");
+      stageBytes_[i] = stageBytes;
+    } else if (stageBytes_[i] < stageBytes) {
+      HIP_OK(hipHostFree(hStage_[i]), "hipHostFree stage");
+      HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hStage_[i]), stageBytes, hipHostMallocDefault),
+             "hipHostMalloc stage");
+      stageBytes_[i] = stageBytes;
+    }
     stageUsed_[i] = false;
   }
+  stageNext_ = 0;
   for (auto& e : packEvents_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
   // fine-grained (coherent) pinned word the marker kernel stores the phase into
   HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hPhase_), 64, hipHostMallocCoherent), "hipHostMalloc phase");
@@ -385,7 +396,7 @@ bool Agent::flushBatch(int nstaged, std::string* err) {
     lastPackHead_ = seq_;
   }
   batches_++;
-  stageNext_ = (stageNext_ + 1) % kStage;
+  stageNext_ = (stageNext_ + 1) % nStage_;
   return true;
 }
 
@@ -430,7 +441,12 @@ void Agent::samplerLoop() {
     }
     // make sure the staging buffer we are about to fill is no longer in flight
     if (staged == 0 && stageUsed_[stageNext_]) {
-      hipWarn(hipEventSynchronize(stageDone_[stageNext_]), "staging buffer wait");
+      if (hipEventQuery(stageDone_[stageNext_]) == hipErrorNotReady) {
+        const uint64_t w0 = monoNs();
+        hipWarn(hipEventSynchronize(stageDone_[stageNext_]), "staging buffer wait");
+        stageWaits_++;
+        stageWaitNs_ += monoNs() - w0;
+      }
       stageUsed_[stageNext_] = false;
     }
     uint8_t* h = hStage_[stageNext_];
@@ -732,6 +748,9 @@ Json Agent::stats() const {
   j["batches"] = static_cast<unsigned long long>(batches_.load());
   j["gathers"] = static_cast<unsigned long long>(gathers_.load());
   j["late_ticks"] = static_cast<unsigned long long>(lateTicks_.load());
+  j["stages"] = nStage_;
+  j["stage_waits"] = static_cast<unsigned long long>(stageWaits_.load());
+  j["stage_wait_ms"] = stageWaitNs_.load() * 1e-6;
   const uint64_t n = samplesTaken_.load();
   j["sample_latency_us_avg"] = n ? latencySumNs_.load() / static_cast<double>(n) * 1e-3 : 0.0;
   j["sample_latency_us_max"] = latencyMaxNs_.load() * 1e-3;

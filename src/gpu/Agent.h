@@ -49,6 +49,7 @@ struct AgentConfig {
   int world = 1;
   double sampleHz = 1000.0;
   int batch = 32;                    // samples per H2D copy + pack launch
+  int stages = 64;                   // pinned staging batches in flight (<= 256)
   uint64_t ringSlots = 1ull << 20;   // 256 MiB of HBM history per GPU
   uint32_t gatherCapSlots = 4096;    // max slots per rank per gather (1 MiB)
   std::string gatherMode = "gather"; // gather | allgather | none
@@ -144,12 +145,19 @@ class Agent {
   bool recvUsed_[kRecv] = {};
   int recvNext_ = 0;
 
-  // host staging (pinned)
-  static constexpr int kStage = 4;
-  uint8_t* hStage_[kStage] = {};
-  hipEvent_t stageDone_[kStage] = {};
-  bool stageUsed_[kStage] = {};
+  // host staging (pinned): cfg_.stages batches may be in flight (H2D copy +
+  // pack) before the sampler waits.  The pack stream can sit behind a long
+  // run-ahead of the trainer's own work when streams share a hardware queue
+  // (GPU_MAX_HW_QUEUES), so the default gives ~2 s of slack at 1 kHz.
+  static constexpr int kMaxStage = 256;
+  uint8_t* hStage_[kMaxStage] = {};
+  hipEvent_t stageDone_[kMaxStage] = {};
+  bool stageUsed_[kMaxStage] = {};
+  size_t stageBytes_[kMaxStage] = {};
   int stageNext_ = 0;
+  int nStage_ = 0;
+  std::atomic<uint64_t> stageWaits_{0};
+  std::atomic<uint64_t> stageWaitNs_{0};
   size_t R_ = 0;
 
   // pack bookkeeping (sampler thread)

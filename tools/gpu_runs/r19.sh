@@ -1,0 +1,8 @@
+# fused ops + fused AdamW: numerics, A/B step time, kernel profile, headline bench
+set -o pipefail
+O=gpurun_out/r19; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_ops_gpu.py > $O/ops.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-agent --optimizer torch > $O/bench_torchopt.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-agent > $O/bench_fused.log 2>&1 && \
+export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o fused -- python3 bench.py --steps 3 --warmup 2 --no-agent > $O/prof.log 2>&1 && \
+timeout -k 10 600 python -u bench.py > $O/bench_headline.log 2>&1
