@@ -52,7 +52,7 @@ def parse_args(argv=None):
                    help="fused: one-launch CDNA4 AdamW (dynolog_amd.ops.optim); torch: AdamW(fused=True)")
     p.add_argument("--host-sync", action="store_true",
                    help="synchronize the device at the end of every step (no host run-ahead)")
-    p.add_argument("--batches", type=int, default=4,
+    p.add_argument("--batches", type=int, default=64,
                    help="distinct synthetic batches cycled through the steps")
     p.add_argument("--phases", action="store_true",
                    help="mark forward/backward/optimizer on the GPU stream and report per-phase metrics")

@@ -51,3 +51,18 @@ def test_attention_forward_peaky_scores(ops):
     ref = _ref(q, k, v, 128 ** -0.5)
     err = (o.float() - ref).abs().max().item()
     assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("B,S,H,KV", [(1, 128, 1, 1), (1, 256, 4, 2), (2, 512, 8, 2), (1, 384, 4, 4)])
+def test_attention_backward(ops, B, S, H, KV):
+    q, k, v = _inputs(B, S, H, KV, seed=7 * S + H)
+    q, k, v = (t.requires_grad_(True) for t in (q, k, v))
+    do = torch.randn(B, S, H, 128, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1)).bfloat16()
+    o = ops.attention(q, k, v)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    _ref(qr, kr, vr, 128 ** -0.5).backward(do.float())
+    for name, a, r in (("dq", q.grad, qr.grad), ("dk", k.grad, kr.grad), ("dv", v.grad, vr.grad)):
+        err = (a.float() - r).abs().max().item()
+        scale = r.abs().max().item()
+        assert err < 2e-2 * max(scale, 1.0), f"{name}: max err {err:.4g} (ref max {scale:.3g})"

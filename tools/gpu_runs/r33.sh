@@ -1,0 +1,7 @@
+# model with CDNA4 flash attention: tests, A/B step time, kernel profile, headline
+set -o pipefail
+O=gpurun_out/r33; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_ops_gpu.py tests/test_attention_gpu.py > $O/tests.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-agent > $O/bench_noagent.log 2>&1 && \
+export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o step -- python3 bench.py --steps 3 --warmup 2 --no-agent > $O/prof.log 2>&1 && \
+timeout -k 10 600 python -u bench.py > $O/bench_headline.log 2>&1
