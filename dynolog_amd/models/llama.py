@@ -110,7 +110,7 @@ class Attention(nn.Module):
                 # CDNA4 flash attention straight on the token-major [B,S,h,hd]
                 # tensors: no transposes in or out
                 o = ops.attention(q, k, v)
-                return self.wo(o.view(b, s, c.n_heads * hd))
+                return ops.linear(o.view(b, s, c.n_heads * hd), self.wo.weight)
             q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
         else:
             q, k, v = qkv.split([c.n_heads * hd, c.n_kv_heads * hd, c.n_kv_heads * hd], -1)
@@ -131,10 +131,10 @@ class FeedForward(nn.Module):
         self.w2 = nn.Linear(cfg.ffn_dim, cfg.d_model, bias=False)
 
     def forward(self, x):
-        gu = self.w13(x)
-        if fused_ops_enabled(gu):
+        if fused_ops_enabled(x):
             from .. import ops
-            return self.w2(ops.swiglu(gu))
+            return ops.linear(ops.swiglu(ops.linear(x, self.w13.weight)), self.w2.weight)
+        gu = self.w13(x)
         g, u = gu.chunk(2, dim=-1)
         return self.w2(F.silu(g) * u)
 

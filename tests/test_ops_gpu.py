@@ -192,3 +192,24 @@ def test_fused_adamw_tracks_torch_fused(ops):
     for a, b in zip(pa, pb):
         diff = (a.float() - b.float()).abs().max().item()
         assert diff <= 2e-2, diff
+
+
+@pytest.mark.parametrize("R,C", [(8192, 4096), (136, 72), (64, 8)])
+def test_transpose2d(ops, R, C):
+    x = torch.randn(R, C, device=DEV).bfloat16()
+    assert torch.equal(ops.transpose2d(x), x.t().contiguous())
+
+
+def test_linear_grads_match_torch(ops):
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(2, 256, 512, device=DEV, generator=g).bfloat16().requires_grad_(True)
+    w = (0.05 * torch.randn(384, 512, device=DEV, generator=g)).bfloat16().requires_grad_(True)
+    dy = torch.randn(2, 256, 384, device=DEV, generator=g).bfloat16()
+    y = ops.linear(x, w)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    (xr @ wr.t()).backward(dy.float())
+    _close(y, xr.detach() @ wr.detach().t(), 1e-2, 2e-2, "linear y")
+    _close(x.grad, xr.grad, 1e-2, 2e-2, "linear dx")
+    _close(w.grad, wr.grad, 1e-2, 5e-2, "linear dw")
