@@ -7,6 +7,7 @@ import os
 import pytest
 import torch
 import torch.nn.functional as F
+import torch.nn.functional as F_
 
 pytestmark = pytest.mark.gpu
 
@@ -213,3 +214,21 @@ def test_linear_grads_match_torch(ops):
     _close(y, xr.detach() @ wr.detach().t(), 1e-2, 2e-2, "linear y")
     _close(x.grad, xr.grad, 1e-2, 2e-2, "linear dx")
     _close(w.grad, wr.grad, 1e-2, 5e-2, "linear dw")
+
+
+@pytest.mark.parametrize("T,D,F", [(256, 256, 512), (128, 128, 192)])
+def test_ffn_matches_fp32(ops, T, D, F):
+    g = torch.Generator(device=DEV).manual_seed(T + F)
+    x = torch.randn(T, D, device=DEV, generator=g).bfloat16().requires_grad_(True)
+    w13 = (D ** -0.5 * torch.randn(2 * F, D, device=DEV, generator=g)).bfloat16().requires_grad_(True)
+    w2 = (F ** -0.5 * torch.randn(D, F, device=DEV, generator=g)).bfloat16().requires_grad_(True)
+    dy = torch.randn(T, D, device=DEV, generator=g).bfloat16()
+    y = ops.ffn(x, w13, w2)
+    y.backward(dy)
+    xr, w13r, w2r = (t.detach().float().requires_grad_(True) for t in (x, w13, w2))
+    a, b = (xr @ w13r.t()).chunk(2, -1)
+    yr = (F_.silu(a) * b) @ w2r.t()
+    yr.backward(dy.float())
+    _close(y, yr, 2e-2, 2e-2, "ffn y")
+    for n, p_, r in (("dx", x, xr), ("dw13", w13, w13r), ("dw2", w2, w2r)):
+        _close(p_.grad, r.grad, 2e-2, 5e-2, f"ffn {n}")
