@@ -232,3 +232,24 @@ def test_ffn_matches_fp32(ops, T, D, F):
     _close(y, yr, 2e-2, 2e-2, "ffn y")
     for n, p_, r in (("dx", x, xr), ("dw13", w13, w13r), ("dw2", w2, w2r)):
         _close(p_.grad, r.grad, 2e-2, 5e-2, f"ffn {n}")
+
+
+@pytest.mark.parametrize("N,D", [(512, 4096), (77, 136)])
+def test_add_rms_norm_fwd_bwd(ops, N, D):
+    g = torch.Generator(device=DEV).manual_seed(N)
+    x = torch.randn(N, D, device=DEV, generator=g).bfloat16().requires_grad_(True)
+    d = torch.randn(N, D, device=DEV, generator=g).bfloat16().requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(D, device=DEV, generator=g)).bfloat16().requires_grad_(True)
+    dh = torch.randn(N, D, device=DEV, generator=g).bfloat16()
+    dy = torch.randn(N, D, device=DEV, generator=g).bfloat16()
+    h, y = ops.add_rms_norm(x, d, w, 1e-5)
+    torch.autograd.backward([h, y], [dh, dy])
+    xr, dr, wr = (t.detach().float().requires_grad_(True) for t in (x, d, w))
+    hr = xr + dr
+    yr = _rms_ref(hr, wr, 1e-5)
+    torch.autograd.backward([hr, yr], [dh.float(), dy.float()])
+    _close(h, hr, 1e-2, 2e-2, "add_rms_norm h")
+    _close(y, yr, 1e-2, 2e-2, "add_rms_norm y")
+    _close(x.grad, xr.grad, 1e-2, 3e-2, "add_rms_norm dx")
+    _close(d.grad, dr.grad, 1e-2, 3e-2, "add_rms_norm ddelta")
+    _close(w.grad, wr.grad, 1e-2, 0.5, "add_rms_norm dw")
