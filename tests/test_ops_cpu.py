@@ -1,0 +1,39 @@
+"""Host-side contract of dynolog_amd.ops (no GPU needed): every op refuses
+non-CUDA / non-bf16 inputs loudly instead of silently falling back, and the
+model keeps its plain PyTorch path for CPU tensors."""
+import pytest
+import torch
+
+from dynolog_amd import ops
+from dynolog_amd.models import llama
+
+
+def _bf(*shape):
+    return torch.zeros(*shape, dtype=torch.bfloat16)
+
+
+@pytest.mark.parametrize("call", [
+    lambda: ops.rms_norm(_bf(4, 8), _bf(8), 1e-5),
+    lambda: ops.add_rms_norm(_bf(4, 8), _bf(4, 8), _bf(8), 1e-5),
+    lambda: ops.swiglu(_bf(4, 32)),
+    lambda: ops.rope_qkv(_bf(1, 4, 3 * 32), torch.zeros(4, 8), torch.zeros(4, 8), 1, 1),
+    lambda: ops.cross_entropy(_bf(4, 16), torch.zeros(4, dtype=torch.long)),
+    lambda: ops.attention(_bf(1, 128, 2, 128), _bf(1, 128, 1, 128), _bf(1, 128, 1, 128)),
+    lambda: ops.linear(_bf(4, 8), _bf(8, 8)),
+    lambda: ops.ffn(_bf(64, 64), _bf(128, 64), _bf(64, 64)),
+    lambda: ops.transpose2d(_bf(8, 8)),
+])
+def test_ops_refuse_cpu_tensors(call):
+    with pytest.raises(TypeError, match="CUDA"):
+        call()
+
+
+def test_model_cpu_path_is_plain_pytorch():
+    torch.manual_seed(0)
+    m = llama.build_llama("tiny", device="cpu", dtype=torch.float32)
+    ids = torch.randint(0, m.cfg.vocab_size, (2, 17))
+    loss = llama.lm_loss(m(ids[:, :-1]), ids[:, 1:])
+    loss.backward()
+    assert torch.isfinite(loss)
+    assert all(p.grad is not None for p in m.parameters())
+    assert not llama.fused_ops_enabled(ids)
