@@ -22,7 +22,14 @@ def step():
 for _ in range(2):
     step()
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+             with_stack=True) as prof:
     step()
     torch.cuda.synchronize()
 print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=45, max_name_column_width=40, max_shapes_column_width=70))
+# the small ATen kernels left between the fused ops, with their callers
+for e in prof.key_averages(group_by_input_shape=True, group_by_stack_n=6):
+    if e.key in ("aten::copy_", "aten::fill_", "aten::zero_", "aten::add", "aten::add_", "aten::to",
+                 "aten::_to_copy", "aten::contiguous", "aten::clone", "aten::zeros", "aten::zeros_like"):
+        print(e.key, e.count, f"{e.device_time_total/1e3:.2f}ms", e.input_shapes[:3])
+        print("   ", " <- ".join(str(f) for f in (e.stack or [])[:6]))
