@@ -98,7 +98,7 @@ def main(argv=None) -> int:
     from dynolog_amd.parallel import dist as pdist
 
     env = pdist.init()
-    dev = torch.device("cuda", env.local_rank)
+    dev = torch.device("cuda", pdist.device_index(env))
     torch.manual_seed(1234 + env.rank)
     torch.backends.cuda.matmul.allow_tf32 = False
 
@@ -123,7 +123,7 @@ def main(argv=None) -> int:
 
     ag = None
     if use_agent:
-        ag = dagent.GpuAgent.start(device=env.local_rank, rank=env.rank, world=env.world,
+        ag = dagent.GpuAgent.start(device=pdist.device_index(env), rank=env.rank, world=env.world,
                                    sample_hz=args.sample_hz, batch=args.pack_batch,
                                    gather_mode=args.gather_mode, log_file=args.log_file,
                                    counter_set=args.counter_set,
@@ -242,7 +242,7 @@ def main(argv=None) -> int:
         "scaling": "weak",
         "vs_baseline": round(value / (BASELINE_SAMPLES_PER_SEC_PER_GPU * env.world), 2),
         "dtype": "bf16",
-        "data": "synthetic (random tokens; random-init Llama-3-8B weights)",
+        "data": f"synthetic (random tokens; random-init {args.model} weights)",
         "config": {
             "model": args.model, "global_batch": B * env.world, "seq_len": S,
             "parallelism": f"dp{env.world}", "sample_hz_target": args.sample_hz,

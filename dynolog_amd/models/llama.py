@@ -57,6 +57,10 @@ CONFIGS = {
     "llama3-8b": LlamaConfig(),
     "llama3-70b": LlamaConfig(d_model=8192, n_layers=80, n_heads=64, n_kv_heads=8,
                               ffn_dim=28672),
+    # head_dim 128 like the 8B, so every fused CDNA4 kernel runs; for multi-rank
+    # rehearsals and tests only (never used for reported numbers)
+    "small": LlamaConfig(vocab_size=2048, d_model=512, n_layers=4, n_heads=4, n_kv_heads=2,
+                         ffn_dim=1024, max_seq_len=4096),
     # tiny config for CPU unit tests only (never used for reported numbers)
     "tiny": LlamaConfig(vocab_size=512, d_model=128, n_layers=2, n_heads=4, n_kv_heads=2,
                         ffn_dim=256, max_seq_len=256),
