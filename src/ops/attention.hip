@@ -82,13 +82,12 @@ __device__ __forceinline__ void consume(const bf16x8& x) { asm volatile("" ::"v"
 // it, which would serialise the prefetch ring; here the kernel waits with
 // counted s_waitcnt vmcnt(N) + barrier itself.  (Compiler-managed global
 // loads stay correct: its own vmcnt waits only get more conservative.)
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
+// (m0 is a reserved register; clang warns about clobbering it, hence the
+// target's -Wno-inline-asm: nothing else in these kernels uses m0.)
 __device__ __forceinline__ void dma16(const void* src, uint32_t lds_addr) {
   asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(src)
                : "memory", "m0");
 }
-#pragma clang diagnostic pop
 
 __device__ __forceinline__ void dma4(const void* src, uint32_t lds_addr) {
   asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(lds_addr), "v"(src)
