@@ -170,7 +170,8 @@ class GpuAgent:
               log_interval_ms: int = 1000, sinks: Sequence[str] = ("json",),
               log_file: str = "", uid: Optional[bytes] = None, process_group=None,
               daemon_endpoint: str = "dynolog", fault_inject: str = "",
-              slot_ring: str = "", stages: int = 64) -> "GpuAgent":
+              slot_ring: str = "", stages: int = 64,
+              force_collective: bool = False) -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
@@ -192,6 +193,8 @@ class GpuAgent:
                    ring_slots=ring_slots, gather_cap_slots=gather_cap_slots,
                    gather_mode=gather_mode, counter_set=counter_set, log_interval_ms=log_interval_ms,
                    sinks=list(sinks), log_file=log_file, daemon_endpoint=daemon_endpoint)
+        if force_collective:  # testing: RCCL gather path with a 1-rank communicator
+            cfg["force_collective"] = True
         if fault_inject:  # testing: "gather_error@N"
             cfg["fault_inject"] = fault_inject
         if slot_ring:  # rank 0: raw slot stream in /dev/shm (utils/slot_ring.py)

@@ -50,6 +50,7 @@ struct AgentConfig {
   double sampleHz = 1000.0;
   int batch = 32;                    // samples per H2D copy + pack launch
   int stages = 64;                   // pinned staging batches in flight (<= 256)
+  bool forceCollective = false;      // testing: use the RCCL path (1-rank comm) at world 1
   uint64_t ringSlots = 1ull << 20;   // 256 MiB of HBM history per GPU
   uint32_t gatherCapSlots = 4096;    // max slots per rank per gather (1 MiB)
   std::string gatherMode = "gather"; // gather | allgather | none
@@ -156,6 +157,7 @@ class Agent {
   size_t stageBytes_[kMaxStage] = {};
   int stageNext_ = 0;
   int nStage_ = 0;
+  bool collective_ = false;  // gathers go through RCCL (world > 1, or forced at world 1)
   std::atomic<uint64_t> stageWaits_{0};
   std::atomic<uint64_t> stageWaitNs_{0};
   size_t R_ = 0;

@@ -247,3 +247,35 @@ def test_slot_ring_raw_stream_in_shm(native_built):
     assert rd["busy"] > 10.0 and rd["pend"] == 0
     assert res["dropped"] == 0
     assert not os.path.exists(f"/dev/shm/{name}.hdr")       # unlinked on stop
+
+
+@pytest.mark.parametrize("mode", ["gather", "allgather"])
+def test_rccl_gather_path_with_one_rank(native_built, mode):
+    """The multi-rank gather code (send buffer, ncclGather / ncclAllGather on
+    the trainer's stream, full-payload drain, per-rank ingest) exercised on a
+    one-GPU box through a 1-rank RCCL communicator (force_collective)."""
+    res = _run(f"""
+        from dynolog_amd import agent
+        agent.preinit()
+        import json, time, torch
+        torch.cuda.set_device(0)
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), gather_mode={mode!r},
+                                 force_collective=True)
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        t0 = agent.mono_ns()
+        for _ in range(40):
+            for _ in range(10):
+                y = x @ x
+            a.step()
+        torch.cuda.synchronize()
+        t1 = agent.mono_ns()
+        a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+        st = a.stats(); wc = a.window_counts(t0, t1)
+        a.stop()
+        print("RESULT " + json.dumps(dict(stats=st, wc=wc, window_s=(t1 - t0) * 1e-9)))
+    """)
+    st = res["stats"]
+    assert st["collective"] is True, st
+    assert st["last_error"] == "" and not st["gather_failed"], st
+    assert st["gathers"] >= 40, st
+    assert res["wc"][0] > 0 and st["ranks"][0]["received"] >= res["wc"][0], st
