@@ -62,6 +62,12 @@ def parse_args(argv=None):
     p.add_argument("--ab-rounds", type=int, default=6,
                    help="interleaved paused/sampling window pairs for the overhead estimate")
     p.add_argument("--ab-steps", type=int, default=5, help="steps per A/B window")
+    p.add_argument("--host-pmu", default="auto", choices=["auto", "off"],
+                   help="co-sample the host CPU PMU (EPYC core/L3/UMC via dynolog "
+                        "--enable_perf_monitor) during the run, paused with the agent in the A/B "
+                        "windows (BASELINE config 5); auto = on when perf_event allows it")
+    p.add_argument("--host-pmu-metrics", default="",
+                   help="metric ids for --host-pmu (default: utils.host_pmu.DEFAULT_METRICS)")
     p.add_argument("--log-file", default="", help="agent log destination (default stderr)")
     p.add_argument("--json-out", default="", help="also write the result line here")
     p.add_argument("--sweep-hz", default="",
@@ -129,6 +135,30 @@ def main(argv=None) -> int:
                                    counter_set=args.counter_set,
                                    sinks=("json", "memory"))
 
+    # Host CPU PMU co-sampler (one daemon per node, on local rank 0), counting
+    # system-wide or, failing that, the ranks of this node.
+    hpmu = None
+    if args.host_pmu != "off":
+        import socket
+        me = (socket.gethostname(), os.getpid())
+        peers = [me]
+        if torch.distributed.is_initialized():
+            peers = [None] * env.world
+            torch.distributed.all_gather_object(peers, me)
+        if env.local_rank == 0:
+            from dynolog_amd.utils.host_pmu import DEFAULT_METRICS, HostPmuCosampler
+            hpmu = HostPmuCosampler(args.host_pmu_metrics or DEFAULT_METRICS).start(
+                [pid for host, pid in peers if host == me[0]])
+
+    def sampling(on: bool) -> None:
+        """Pause / resume every sampler (GPU agent + host PMU) together."""
+        if on:
+            ag.resume()
+        else:
+            ag.pause()
+        if hpmu is not None:
+            hpmu.set_enabled(on)
+
     last_loss = [0.0]
     import contextlib
     use_phases = ag is not None and args.phases
@@ -173,10 +203,10 @@ def main(argv=None) -> int:
     base_s = None
     pooled_active_s = None
     if ag is not None and not args.skip_baseline:
-        ag.pause()
+        sampling(False)
         time.sleep(0.05)
         base_s, _, _ = timed(args.steps)
-        ag.resume()
+        sampling(True)
         for _ in range(2):  # let sampling re-settle outside the window
             train_step()
         torch.cuda.synchronize()
@@ -205,7 +235,7 @@ def main(argv=None) -> int:
             # MI355X sclk swings ~5% under its power cap (visible in the
             # agent's own sclk_mhz), so a single A/B pair cannot resolve a
             # sub-1% overhead; pooling all windows can.
-            ag.pause()
+            sampling(False)
             time.sleep(0.05)
             base2_s, _, _ = timed(args.steps)
             paused_s, paused_n = base_s + base2_s, 2 * args.steps
@@ -213,17 +243,17 @@ def main(argv=None) -> int:
             for r in range(args.ab_rounds):
                 for want_active in ((True, False) if r % 2 == 0 else (False, True)):
                     if want_active:
-                        ag.resume()
+                        sampling(True)
                         train_step()
                         torch.cuda.synchronize()
                         s, _, _ = timed(args.ab_steps)
                         active_s, active_n = active_s + s, active_n + args.ab_steps
-                        ag.pause()
+                        sampling(False)
                         time.sleep(0.02)
                     else:
                         s, _, _ = timed(args.ab_steps)
                         paused_s, paused_n = paused_s + s, paused_n + args.ab_steps
-            ag.resume()
+            sampling(True)
             base_s = paused_s / paused_n * args.steps
             pooled_active_s = active_s / active_n * args.steps
 
@@ -267,6 +297,8 @@ def main(argv=None) -> int:
                         ("samples_taken", "samples_failed", "sample_latency_us_avg",
                          "sample_latency_us_max", "late_ticks", "stage_waits", "stage_wait_ms",
                          "gathers", "raw_instances", "last_error")}
+    if hpmu is not None and env.rank == 0:
+        out["host_pmu"] = hpmu.summary()
     if use_phases and env.rank == 0:
         keep = ("samples", "gpu_busy_pct", "mfma_util", "mfma_bf16_tflops", "hbm_read_gbps",
                 "hbm_write_gbps", "lds_bank_conflict_rate", "occupancy_pct")
@@ -311,6 +343,8 @@ def main(argv=None) -> int:
                           indent=1)
     if ag is not None:
         ag.stop()
+    if hpmu is not None:
+        hpmu.stop()
     pdist.shutdown()
     return 0
 

@@ -71,9 +71,25 @@ bool PerfMonitor::init(std::string* err) {
   return !active_.empty();
 }
 
+void PerfMonitor::setEnabled(bool on) {
+  std::lock_guard<std::mutex> g(stepMu_);
+  if (on == enabled_.load()) return;
+  if (on) {
+    mon_.enable();
+  } else {
+    mon_.disable();
+  }
+  enabled_ = on;
+}
+
 void PerfMonitor::step() {
+  std::lock_guard<std::mutex> g(stepMu_);
   std::map<std::string, double> en;
   mux_.clear();
+  if (!enabled_) {
+    outputs_.clear();
+    return;
+  }
   auto counts = mon_.readAllCounts(&mux_, &en);
   outputs_.clear();
   std::map<std::string, int> cpusOf;
@@ -87,7 +103,8 @@ void PerfMonitor::step() {
 }
 
 void PerfMonitor::log(Logger& logger) {
-  logger.setTimestamp();  // reference never sets one (README.md:203-205 shows 1969 dates)
+  logger.setTimestamp();
+  if (target_.pid >= 0) logger.logInt("pid", target_.pid);  // reference never sets one (README.md:203-205 shows 1969 dates)
   for (const auto& [k, v] : outputs_) logger.logFloat(k, static_cast<float>(v));
   for (const auto& [id, r] : mux_)
     if (r < 0.999) logger.logFloat(id + "_mux_ratio", static_cast<float>(r));

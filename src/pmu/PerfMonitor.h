@@ -8,7 +8,9 @@
 // perf_event_paranoid) are dropped individually with a warning.
 #pragma once
 
+#include <atomic>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <vector>
@@ -26,8 +28,16 @@ class PerfMonitor {
               Target target = Target::systemWide());
   // Opens every metric it can; false if none could be opened.
   bool init(std::string* err);
+  // One reporting interval: read, derive, rotate the mux group.  No-op while
+  // paused (outputs cleared, nothing to log).
   void step();
   void log(Logger& logger);
+  // Pause / resume counting (the `setPerfMonitor` RPC).  Paused counters do
+  // not run, so the first interval after a resume covers enabled time only
+  // (rates divide by time_enabled).  Used to A/B the PMU's own cost.
+  void setEnabled(bool on);
+  bool enabled() const { return enabled_.load(); }
+  int pid() const { return target_.pid; }
   const std::vector<std::string>& activeMetrics() const { return active_; }
   const std::map<std::string, double>& lastOutputs() const { return outputs_; }
 
@@ -40,6 +50,8 @@ class PerfMonitor {
   Monitor mon_;
   std::map<std::string, double> outputs_;
   std::map<std::string, double> mux_;
+  std::atomic<bool> enabled_{true};
+  std::mutex stepMu_;
 };
 
 std::shared_ptr<PmuDeviceManager> getDefaultPmuDeviceManager();

@@ -242,3 +242,63 @@ def test_metric_stats_rpc_and_cli(native_built, daemon):
     st = json.loads(r.stdout)
     assert st["key"] == "uptime" and st["count"] >= 1
     assert daemon.rpc({"fn": "getMetricStats"})["status"] == "failed"
+
+
+def test_set_perf_monitor_rpc_pause_resume_per_pid(native_built):
+    """setPerfMonitor pauses / resumes the CPU PMU collector (no records while
+    paused); --perf_monitor_pids counts named processes, one record per pid."""
+    with DaemonProcess(["--enable_perf_monitor", "--perf_monitor_reporting_interval_s=1",
+                        f"--perf_monitor_pids={os.getpid()}", "--perf_monitor_mux=false",
+                        "--perf_monitor_metrics=cpu_clock,page_faults"]) as d:
+        st = d.rpc({"fn": "setPerfMonitor"})
+        if st["status"] != "ok":
+            pytest.skip("per-process perf_event unavailable: " + st["status"])
+        assert st["enabled"] is True and st["pids"] == [os.getpid()]
+        assert sorted(st["active"]) == ["cpu_clock", "page_faults"]
+        t0 = time.time()
+        while time.time() - t0 < 2.4:
+            _ = [bytearray(1 << 20) for _ in range(4)]
+        assert d.rpc({"fn": "setPerfMonitor", "enable": False})["enabled"] is False
+        n0 = len(d.rpc({"fn": "getMetrics", "collector": "perf", "last": 100})["records"])
+        time.sleep(2.2)
+        recs = d.rpc({"fn": "getMetrics", "collector": "perf", "last": 100})["records"]
+        assert len(recs) == n0                      # paused: no ticks logged
+        assert all(r["pid"] == os.getpid() for r in recs)
+        busy = [r for r in recs if "cpu_clock_ms_per_s" in r]
+        assert busy and max(r["cpu_clock_ms_per_s"] for r in busy) > 300  # this loop was busy
+        assert max(r.get("page_faults_per_s", 0) for r in recs) > 0
+        assert d.rpc({"fn": "setPerfMonitor", "enable": True})["enabled"] is True
+        time.sleep(1.5)
+        assert len(d.rpc({"fn": "getMetrics", "collector": "perf", "last": 100})["records"]) > n0
+
+
+def test_set_perf_monitor_reports_why_unavailable(native_built):
+    with DaemonProcess(["--enable_perf_monitor", "--perf_monitor_metrics=no_such_metric"]) as d:
+        assert d.rpc({"fn": "setPerfMonitor"})["status"].startswith("unavailable: ")
+    with DaemonProcess([]) as d:
+        assert d.rpc({"fn": "setPerfMonitor", "enable": True})["status"] == \
+            "unavailable: perf monitor not enabled"
+
+
+def test_host_pmu_cosampler_summary(native_built):
+    """bench.py's host PMU co-sampler (BASELINE config 5 plumbing): falls back
+    from system-wide to per-process, summarises means + mux ratios, and never
+    raises when perf_event is closed."""
+    from dynolog_amd.utils.host_pmu import HostPmuCosampler
+    s = HostPmuCosampler("cpu_clock,page_faults,context_switches").start([os.getpid()])
+    try:
+        if not s.running:
+            pytest.skip("perf_event unavailable: " + s.reason)
+        assert s.mode in ("system-wide", "per-process")
+        t0 = time.time()
+        while time.time() - t0 < 2.5:
+            _ = [bytearray(1 << 20) for _ in range(4)]
+        sm = s.summary()
+        assert sm["status"] == "ok" and sm["records"] >= 2
+        assert sm["mean"]["cpu_clock_ms_per_s"] > 100
+        assert set(sm["active_metrics"]) == {"cpu_clock", "page_faults", "context_switches"}
+    finally:
+        s.stop()
+    bad = HostPmuCosampler("no_such_metric").start([os.getpid()])
+    assert not bad.running and bad.summary()["status"] == "unavailable"
+    assert "unavailable" in bad.summary()["reason"]
