@@ -36,6 +36,8 @@
 
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace {
 
 typedef unsigned short u16;
@@ -179,9 +181,105 @@ struct Stage {
 // per tile.  Per wave and key tile: S^T = K Q^T (2 x 8 MFMAs; query on the
 // lane, keys in registers), online softmax per lane, O^T += V^T P^T (4 d-tiles
 // x 4 MFMAs, P^T straight from the S^T accumulators, V^T by transposed reads).
+// Per-tile VALU trimmed (r69/r70, +14 % vs the first version): causal-mask
+// selects only in the tiles that cross a wave's diagonal (separate loop +
+// instantiation), scale folded into the exp2 argument's fma, row max via
+// v_max3 without hipcc's canonicalising v_max, half-wave reductions with
+// v_permlane32_swap instead of ds_bpermute, O rescale skipped when no lane's
+// running max moved (exact).
 constexpr int FQ = 256, FK = 64, FW = 8, FSTAGES = 4;
 constexpr int FTILE = FK * ROWB;  // one K or V tile image, 16 KiB
 constexpr int FNT = 64 * FW;
+
+// Combine the two half-wave values of a query row (lanes l and l + 32):
+// v_permlane32_swap(x, x) leaves {own, partner} in its two results on both
+// halves, so one swap + one VALU op replaces a ds_bpermute round trip.
+__device__ __forceinline__ float pair_max(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+// v_max3_f32 without the canonicalising v_max hipcc puts in front of fmaxf
+// on MFMA results (NaN-quieting; scores are never sNaN).
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// One key tile of the forward for one wave: S^T = K Q^T, online softmax in
+// the exp2 domain (running max m is kept pre-scaled; the row max is taken on
+// the raw scores, c > 0, and p = exp2(c*s - m) is one fma + one exp), then
+// O^T += V^T P^T.  DIAG: the tile crosses the wave's causal diagonal.
+template <bool DIAG>
+__device__ __forceinline__ void fwd_tile(const unsigned char* kt, const unsigned char* vt,
+                                         const bf16x8 (&qf)[8], f32x16 (&oacc)[4], float& m,
+                                         float& l, int k0, int qrow, int h, int col, int lane,
+                                         float c) {
+  f32x16 s0 = zero16(), s1 = zero16();
+  bf16x8 ka[8], kb2[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    ka[s] = row_read(kt, col, 2 * s + h);
+    kb2[s] = row_read(kt, col + 32, 2 * s + h);
+  }
+  // s0's chain first, then s1's: the row max over s0 runs on the VALU
+  // under s1's MFMAs instead of after both chains.
+#pragma unroll
+  for (int s = 0; s < 8; ++s) s0 = mfma(ka[s], qf[s], s0);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) s1 = mfma(kb2[s], qf[s], s1);
+  float ma = -INFINITY, mb = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    if constexpr (DIAG) {
+      const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (key > qrow) s0[r] = -INFINITY;
+      if (key + 1 > qrow) s0[r + 1] = -INFINITY;
+    }
+    ma = max3(ma, s0[r], s0[r + 1]);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    if constexpr (DIAG) {
+      const int key = k0 + 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (key > qrow) s1[r] = -INFINITY;
+      if (key + 1 > qrow) s1[r + 1] = -INFINITY;
+    }
+    mb = max3(mb, s1[r], s1[r + 1]);
+  }
+  const float mt = fmaxf(ma, mb);
+  const float mn = fmaxf(m, pair_max(mt) * c);  // finite: key tile 0 always has an unmasked key
+  const float alpha = ex2(m - mn);
+  m = mn;
+  float rs = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    s0[r] = ex2(__builtin_fmaf(s0[r], c, -mn));
+    s1[r] = ex2(__builtin_fmaf(s1[r], c, -mn));
+    rs += s0[r] + s1[r];
+  }
+  l = l * alpha + rs;
+  // alpha == 1 in every lane (no row max moved; the common case once the
+  // first tiles are in) skips the O rescale: exact, wave-uniform branch.
+  if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
+  }
+  bf16x8 pb[4] = {acc_operand(s0, 0), acc_operand(s0, 1), acc_operand(s1, 0), acc_operand(s1, 1)};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma(tr_read(vt, 16 * ks, 32 * dt, lane), pb[ks], oacc[dt]);
+}
 
 __global__ __launch_bounds__(FNT, 1) void attn_fwd_kernel(
     const u16* __restrict__ q, const u16* __restrict__ k, const u16* __restrict__ v,
@@ -228,7 +326,8 @@ __global__ __launch_bounds__(FNT, 1) void attn_fwd_kernel(
   for (int t = 0; t < FSTAGES - 1; ++t)
     if (t < ntiles) issue(t);
 
-  for (int t = 0; t < ntiles; ++t) {
+  // One tile step: wait for its DMA, barrier, refill the ring, compute.
+  auto step = [&](int t, auto diag_c) {
     const int k0 = t * FK;
     // this tile landed (the newer ones may stay in flight) ...
     const int newer = ntiles - 1 - t;
@@ -240,61 +339,18 @@ __global__ __launch_bounds__(FNT, 1) void attn_fwd_kernel(
     if (t + FSTAGES - 1 < ntiles) issue(t + FSTAGES - 1);
     const unsigned char* kt = smem + (t & (FSTAGES - 1)) * 2 * FTILE;
     const unsigned char* vt = kt + FTILE;
-    if (active && k0 <= qw0 + 31) {  // wave-uniform: skip tiles wholly above this wave's rows
-      f32x16 s0 = zero16(), s1 = zero16();
-      bf16x8 ka[8], kb2[8];
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        ka[s] = row_read(kt, col, 2 * s + h);
-        kb2[s] = row_read(kt, col + 32, 2 * s + h);
-      }
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        s0 = mfma(ka[s], qf[s], s0);
-        s1 = mfma(kb2[s], qf[s], s1);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
-      const bool diag = k0 + FK - 1 > qw0;
-      float mt = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float x0 = s0[r] * c, x1 = s1[r] * c;
-        if (diag) {
-          if (key > qrow) x0 = -INFINITY;
-          if (key + 32 > qrow) x1 = -INFINITY;
-        }
-        s0[r] = x0;
-        s1[r] = x1;
-        mt = fmaxf(mt, fmaxf(x0, x1));
-      }
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m, mt);  // finite: key tile 0 always has an unmasked key
-      const float alpha = ex2(m - mn);
-      m = mn;
-      float rs = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s0[r] = ex2(s0[r] - mn);
-        s1[r] = ex2(s1[r] - mn);
-        rs += s0[r] + s1[r];
-      }
-      l = l * alpha + rs;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
-      bf16x8 pb[4] = {acc_operand(s0, 0), acc_operand(s0, 1), acc_operand(s1, 0), acc_operand(s1, 1)};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma(tr_read(vt, 16 * ks, 32 * dt, lane), pb[ks], oacc[dt]);
-    }
-  }
+    if (active && k0 <= qw0 + 31)  // wave-uniform: skip tiles wholly above this wave's rows
+      fwd_tile<decltype(diag_c)::value>(kt, vt, qf, oacc, m, l, k0, qrow, h, col, lane, c);
+  };
+  // Only the tiles that cross this wave's causal diagonal pay for the mask:
+  // two loops over one tile sequence, split per wave.  Every wave still runs
+  // all ntiles steps (same barrier count), only the instantiation differs.
+  const int tdiag = min(ntiles, max(0, (qw0 + 1) / FK));  // first tile with k0 + FK - 1 > qw0
+  for (int t = 0; t < tdiag; ++t) step(t, std::false_type{});
+  for (int t = tdiag; t < ntiles; ++t) step(t, std::true_type{});
 
   if (!active) return;
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = pair_sum(l);
   const float inv = 1.f / lt;
   u16* op = o + ((size_t)(b * S + qrow) * H + head) * HD;
 #pragma unroll
