@@ -205,12 +205,15 @@ __device__ __forceinline__ float pair_sum(float x) {
   return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
-// v_max3_f32 without the canonicalising v_max hipcc puts in front of fmaxf
-// on MFMA results (NaN-quieting; scores are never sNaN).
+// max(a, max(b, c)) as v_maximum3_f32 (gfx950): fmaxf on MFMA results makes
+// hipcc quiet each input with a canonicalising v_max first (IEEE mode); the
+// NaN-propagating maximum needs none, and scores are never NaN.  (An
+// inline-asm v_max3 did the same faster but hid the MFMA-result read from
+// hipcc's hazard recognizer: it read accumulators before the MFMA had
+// written them, and outputs varied run to run -- tools/probes/
+// attn_determinism.py, r73.)
 __device__ __forceinline__ float max3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_elementwise_maximum(a, __builtin_elementwise_maximum(b, c));
 }
 
 // One key tile of the forward for one wave: S^T = K Q^T, online softmax in
