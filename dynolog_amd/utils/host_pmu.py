@@ -37,7 +37,6 @@ class HostPmuCosampler:
         self.mode: Optional[str] = None
         self.reason = ""
         self.active: list = []
-        self._paused_records = 0
 
     def _start(self, extra: Sequence[str]):
         from dynolog_amd.utils.daemon import DaemonProcess
@@ -89,9 +88,13 @@ class HostPmuCosampler:
         return list(r.get("records", []))
 
     def summary(self) -> dict:
+        """Never raises (the caller prints its result line right after)."""
         if self.daemon is None:
             return {"status": "unavailable", "reason": self.reason}
-        recs = self.records()
+        try:
+            recs = self.records()
+        except Exception as e:  # noqa: BLE001 - e.g. the daemon died mid-run
+            return {"status": "failed", "mode": self.mode, "reason": f"records: {e}"}
         sums, counts = collections.defaultdict(float), collections.Counter()
         for r in recs:
             for k, v in r.items():
