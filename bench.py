@@ -344,7 +344,10 @@ def main(argv=None) -> int:
     if ag is not None:
         ag.stop()
     if hpmu is not None:
-        hpmu.stop()
+        try:
+            hpmu.stop()
+        except Exception as e:  # noqa: BLE001 - the result line is already out
+            print(f"host PMU co-sampler stop: {e}", file=sys.stderr)
     pdist.shutdown()
     return 0
 
