@@ -24,14 +24,18 @@ from __future__ import annotations
 
 import collections
 import math
+import time
 from typing import Optional, Sequence
 
 DEFAULT_METRICS = ("instructions,cycles,l2_cache_misses,tlb_misses,l3_cache,dram_bandwidth")
 
 
 class HostPmuCosampler:
-    def __init__(self, metrics: str = DEFAULT_METRICS, interval_s: int = 1):
+    def __init__(self, metrics: str = DEFAULT_METRICS, interval_s: int = 1,
+                 extra_args: Sequence[str] = (), start_timeout_s: float = 30.0):
         self.metrics = metrics
+        self.extra_args = list(extra_args)
+        self.start_timeout_s = start_timeout_s
         self.interval_s = max(1, int(interval_s))
         self.daemon = None
         self.mode: Optional[str] = None
@@ -42,9 +46,16 @@ class HostPmuCosampler:
         from dynolog_amd.utils.daemon import DaemonProcess
         d = DaemonProcess(["--enable_perf_monitor", "--perf_monitor_mux=false",
                            "--perf_monitor_reporting_interval_s", str(self.interval_s),
-                           "--perf_monitor_metrics", self.metrics, *extra])
+                           "--perf_monitor_metrics", self.metrics, *self.extra_args, *extra])
         d.start()
-        st = d.rpc({"fn": "setPerfMonitor"}) or {}
+        # "starting": the daemon serves RPCs before its counters are open
+        # (opening system-wide groups on every CPU takes a while); poll.
+        deadline = time.monotonic() + self.start_timeout_s
+        while True:
+            st = d.rpc({"fn": "setPerfMonitor"}) or {}
+            if st.get("status") != "starting" or time.monotonic() > deadline:
+                break
+            time.sleep(0.05)
         if st.get("status") == "ok":
             return d, st
         d.stop()

@@ -182,6 +182,9 @@ bool Daemon::start(std::string* err) {
     *err = server_->error();
     return false;
   }
+  // Anything the RPC surface reports on must be in a defined state before the
+  // first request is served (the perf monitor opens its counters below).
+  if (FLAGS_enable_perf_monitor) markPerfMonitorStarting();
   server_->run();
 
   if (FLAGS_enable_ipc_monitor) {

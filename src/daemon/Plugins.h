@@ -11,6 +11,10 @@ namespace rpc {
 class RpcDispatcher;
 }
 
+// Called before the RPC server starts serving when --enable_perf_monitor is
+// set: until startPerfMonitor() has opened (or failed to open) its counters,
+// setPerfMonitor answers {"status":"starting"} instead of "not enabled".
+void markPerfMonitorStarting();
 void startPerfMonitor(Daemon& d);
 // Shared always-on counters published in shm (pmu/SharedCounters.h).
 void startSharedCounters(Daemon& d);

@@ -1,5 +1,6 @@
 #include "pmu/PerfEvents.h"
 
+#include <dirent.h>
 #include <linux/perf_event.h>
 #include <sys/ioctl.h>
 #include <sys/syscall.h>
@@ -52,6 +53,19 @@ std::string perfOpenErrorHint(int err) {
     case EBUSY: return "PMU busy (exclusive user)";
     default: return strerror(err);
   }
+}
+
+std::vector<int> listThreads(int pid) {
+  std::vector<int> tids;
+  const std::string dir = "/proc/" + std::to_string(pid) + "/task";
+  if (DIR* d = opendir(dir.c_str())) {
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] >= '0' && e->d_name[0] <= '9') tids.push_back(atoi(e->d_name));
+    }
+    closedir(d);
+  }
+  std::sort(tids.begin(), tids.end());
+  return tids;
 }
 
 // ------------------------------------------------------------- EventGroup
@@ -134,7 +148,7 @@ bool EventGroup::readDelta(CountDelta* out) {
 // ------------------------------------------------------------- CountReader
 CountReader::CountReader(std::shared_ptr<MetricDesc> metric, const PmuDeviceManager& mgr,
                          const CpuSet& cpus, Target target, std::string* err)
-    : metric_(std::move(metric)) {
+    : metric_(std::move(metric)), target_(target) {
   const auto* refs = metric_->eventsFor(mgr.arch());
   if (!refs) {
     if (err) *err = "metric " + metric_->id + " unsupported on arch " + cpuArchName(mgr.arch());
@@ -158,12 +172,17 @@ CountReader::CountReader(std::shared_ptr<MetricDesc> metric, const PmuDeviceMana
       byPmu[key].push_back(c);
     }
   }
+  const bool perThread = target.pid >= 0 && target.cgroupFd < 0 && target.allThreads;
   for (auto& [pmuKey, evs] : byPmu) {
     std::vector<std::string> nicks;
     for (const auto& e : evs) nicks.push_back(e.name.substr(0, e.name.find('@')));
+    if (perThread) {
+      perThreadEvs_.emplace_back(evs, nicks);
+      continue;
+    }
     std::vector<int> cpuList;
     if (target.pid >= 0 && target.cgroupFd < 0) {
-      cpuList = {-1};  // per-process: follow the task on any CPU
+      cpuList = {-1};  // one task: follow it on any CPU
     } else if (evs[0].cpumask) {
       cpuList = evs[0].cpumask->cpus();  // uncore: one CPU per package/die
     } else {
@@ -173,26 +192,76 @@ CountReader::CountReader(std::shared_ptr<MetricDesc> metric, const PmuDeviceMana
     for (int c : cpuList) {
       groups_.push_back(std::make_unique<EventGroup>(c, target, evs));
       nicknames_.push_back(nicks);
+      groupTid_.push_back(-1);
+      groupExited_.push_back(false);
     }
+  }
+  if (perThread) {
+    tids_ = listThreads(target.pid);
+    if (tids_.empty()) {
+      if (err) *err = "process " + std::to_string(target.pid) + " not found";
+      return;
+    }
+    for (int tid : tids_) addGroupsFor(tid);
   }
   if (target.pid >= 0) nCoreCpus_ = 1;
 }
 
+void CountReader::addGroupsFor(int tid) {
+  for (const auto& [evs, nicks] : perThreadEvs_) {
+    groups_.push_back(std::make_unique<EventGroup>(-1, Target::thread(tid), evs));
+    nicknames_.push_back(nicks);
+    groupTid_.push_back(tid);
+    groupExited_.push_back(false);
+  }
+}
+
+int CountReader::rescanThreads() {
+  if (perThreadEvs_.empty()) return 0;
+  const auto now = listThreads(target_.pid);
+  // exited threads: their fds still read the final counts; read() retires them
+  for (size_t gi = 0; gi < groups_.size(); ++gi)
+    if (groupTid_[gi] >= 0 && !std::binary_search(now.begin(), now.end(), groupTid_[gi]))
+      groupExited_[gi] = true;
+  for (int tid : now) {
+    if (std::binary_search(tids_.begin(), tids_.end(), tid)) continue;
+    const size_t first = groups_.size();
+    addGroupsFor(tid);
+    if (!opened_) continue;
+    for (size_t gi = first; gi < groups_.size(); ++gi) {
+      std::string e;
+      if (!groups_[gi]->open(pinned_, &e)) {
+        groupExited_[gi] = true;  // raced with the thread's exit (ESRCH): drop it
+        continue;
+      }
+      groups_[gi]->zeroBase();  // count from open: the thread's whole life in this interval
+      if (enabled_) groups_[gi]->enable();
+    }
+  }
+  tids_ = now;
+  return static_cast<int>(tids_.size());
+}
+
 bool CountReader::open(bool pinned, std::string* err) {
+  pinned_ = pinned;
   for (auto& g : groups_)
     if (!g->open(pinned, err)) {
       close();
       return false;
     }
+  opened_ = true;
   return true;
 }
 void CountReader::enable() {
+  enabled_ = true;
   for (auto& g : groups_) g->enable();
 }
 void CountReader::disable() {
+  enabled_ = false;
   for (auto& g : groups_) g->disable();
 }
 void CountReader::close() {
+  opened_ = enabled_ = false;
   for (auto& g : groups_) g->close();
 }
 void CountReader::rebase() {
@@ -202,6 +271,12 @@ void CountReader::rebase() {
 void EventGroup::rebase() {
   GroupRead cur;
   if (read(&cur)) prev_ = cur;
+}
+
+void EventGroup::zeroBase() {
+  GroupRead z;
+  z.values.assign(events_.size(), 0);
+  prev_ = z;
 }
 
 bool CountReader::read(std::map<std::string, double>* counts, double* minMux,
@@ -216,6 +291,14 @@ bool CountReader::read(std::map<std::string, double>* counts, double* minMux,
     enabledMax = std::max(enabledMax, d.enabledNs);
     mux = std::min(mux, d.multiplexRatio());
     for (size_t i = 0; i < d.scaled.size(); ++i) (*counts)[nicknames_[gi][i]] += d.scaled[i];
+  }
+  // retire groups of exited threads now that their final counts are in
+  for (size_t gi = groups_.size(); gi-- > 0;) {
+    if (!groupExited_[gi]) continue;
+    groups_.erase(groups_.begin() + static_cast<long>(gi));
+    nicknames_.erase(nicknames_.begin() + static_cast<long>(gi));
+    groupTid_.erase(groupTid_.begin() + static_cast<long>(gi));
+    groupExited_.erase(groupExited_.begin() + static_cast<long>(gi));
   }
   if (minMux) *minMux = any ? mux : 0.0;
   if (enabledSec) *enabledSec = enabledMax * 1e-9;
@@ -311,6 +394,14 @@ std::map<std::string, std::map<std::string, double>> Monitor::readAllCounts(
     }
   }
   return out;
+}
+
+int Monitor::rescanThreads() {
+  std::lock_guard<std::mutex> g(mu_);
+  int n = 0;
+  for (auto& [name, rs] : groups_)
+    for (auto& r : rs) n = std::max(n, r->rescanThreads());
+  return n;
 }
 
 std::vector<CountReader*> Monitor::readers() {

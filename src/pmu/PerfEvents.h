@@ -40,8 +40,15 @@ struct CountDelta {
 struct Target {
   int pid = -1;      // -1 = all processes (system-wide, needs cpu >= 0)
   int cgroupFd = -1; // >= 0: cgroup mode (pid field carries the fd)
+  // Process targets: count every thread of the process (one group per tid
+  // from /proc/<pid>/task, rescanned by CountReader::rescanThreads()).  A
+  // perf event on pid P with inherit=0 counts only the thread whose tid is P,
+  // which misses a training rank's RCCL proxy, HIP, sampler and dataloader
+  // threads.  false = exactly the task `pid` (a tid, e.g. sampling side bands).
+  bool allThreads = false;
   static Target systemWide() { return Target{}; }
-  static Target process(int pid) { return Target{pid, -1}; }
+  static Target process(int pid) { return Target{pid, -1, true}; }
+  static Target thread(int tid) { return Target{tid, -1, false}; }
 };
 
 // One event group (leader + members) on one CPU (or any CPU for a pid target).
@@ -63,6 +70,9 @@ class EventGroup {
   bool readDelta(CountDelta* out);
   // Reset the delta baseline to the current counter values.
   void rebase();
+  // Baseline = zero counts, so the next readDelta() covers everything since
+  // open() (groups opened mid-interval for a newly seen thread).
+  void zeroBase();
   const std::vector<EventConf>& events() const { return events_; }
   int cpu() const { return cpu_; }
 
@@ -90,16 +100,31 @@ class CountReader {
   // counted during the interval. *enabledSec = time the groups were enabled.
   bool read(std::map<std::string, double>* counts, double* minMuxRatio,
             double* enabledSec = nullptr);
+  // Process targets: open groups for threads that appeared since the last
+  // scan (counting from their open) and retire groups of exited threads
+  // after their final counts were read.  Returns the number of live threads.
+  int rescanThreads();
+  int numThreads() const { return static_cast<int>(tids_.size()); }
   std::shared_ptr<MetricDesc> metric() const { return metric_; }
   int numCpus() const { return nCoreCpus_; }
   size_t numGroups() const { return groups_.size(); }
 
  private:
+  void addGroupsFor(int tid);
   std::shared_ptr<MetricDesc> metric_;
+  Target target_;
   std::vector<std::unique_ptr<EventGroup>> groups_;
   std::vector<std::vector<std::string>> nicknames_;  // per group, per event
+  std::vector<int> groupTid_;                         // per group: tid (process targets) or -1
+  std::vector<bool> groupExited_;                     // per group: read once more, then close
+  std::vector<std::pair<std::vector<EventConf>, std::vector<std::string>>> perThreadEvs_;
+  std::vector<int> tids_;
+  bool opened_ = false, pinned_ = false, enabled_ = false;
   int nCoreCpus_ = 0;
 };
+
+// Thread ids of a process (/proc/<pid>/task), sorted; empty if it is gone.
+std::vector<int> listThreads(int pid);
 
 // Registry + state machine over count readers with time-multiplexed groups
 // (only the front mux group is enabled; muxRotate() advances it).
@@ -119,6 +144,9 @@ class Monitor {
       std::map<std::string, double>* enabledSec = nullptr);
   std::vector<CountReader*> readers();
   size_t numMuxGroups() const { return muxOrder_.size(); }
+  // Per-thread process targets: pick up new / retire exited threads in every
+  // reader; returns the live thread count (0 for other targets).
+  int rescanThreads();
 
  private:
   void enableFront();

@@ -38,6 +38,8 @@ class PerfMonitor {
   void setEnabled(bool on);
   bool enabled() const { return enabled_.load(); }
   int pid() const { return target_.pid; }
+  // Process targets: threads counted in the last interval (0 otherwise).
+  int threads() const { return threads_; }
   const std::vector<std::string>& activeMetrics() const { return active_; }
   const std::map<std::string, double>& lastOutputs() const { return outputs_; }
 
@@ -51,6 +53,8 @@ class PerfMonitor {
   std::map<std::string, double> outputs_;
   std::map<std::string, double> mux_;
   std::atomic<bool> enabled_{true};
+  uint64_t lastStepNs_ = 0;
+  int threads_ = 0;
   std::mutex stepMu_;
 };
 

@@ -434,15 +434,7 @@ int ringCountFor(const CpuSet& cpus) {
 // mmap an inherited cpu=-1 event), so a process target is followed by one
 // event group per existing thread.
 std::vector<int> listTasks(int pid) {
-  std::vector<int> tids;
-  const std::string dir = "/proc/" + std::to_string(pid) + "/task";
-  if (DIR* d = opendir(dir.c_str())) {
-    while (dirent* e = readdir(d)) {
-      if (e->d_name[0] >= '0' && e->d_name[0] <= '9') tids.push_back(atoi(e->d_name));
-    }
-    closedir(d);
-  }
-  std::sort(tids.begin(), tids.end());
+  auto tids = listThreads(pid);
   if (tids.empty()) tids.push_back(pid);
   return tids;
 }
@@ -495,7 +487,7 @@ CountSampleGenerator::CountSampleGenerator(const CpuSet& cpus, Target target,
       for (int c : cpus.cpus()) groups_.push_back(std::make_unique<SamplingGroup>(c, target, events, conf));
     } else {
       for (int tid : listTasks(target.pid))
-        groups_.push_back(std::make_unique<SamplingGroup>(-1, Target::process(tid), events, conf));
+        groups_.push_back(std::make_unique<SamplingGroup>(-1, Target::thread(tid), events, conf));
     }
   } else {
     for (int c : cpus.cpus()) groups_.push_back(std::make_unique<SamplingGroup>(c, target, events, conf));
@@ -627,7 +619,7 @@ ThreadSwitchGenerator::ThreadSwitchGenerator(const CpuSet& cpus, Target target, 
     // Per-task events cannot be inherited *and* mmapped, so follow every
     // existing thread of the process individually.
     for (int tid : listTasks(target.pid)) {
-      groups_.push_back(makeDummyGroup(-1, Target::process(tid), c));
+      groups_.push_back(makeDummyGroup(-1, Target::thread(tid), c));
       ++nRings;
     }
   } else {

@@ -274,10 +274,36 @@ def test_set_perf_monitor_rpc_pause_resume_per_pid(native_built):
 
 def test_set_perf_monitor_reports_why_unavailable(native_built):
     with DaemonProcess(["--enable_perf_monitor", "--perf_monitor_metrics=no_such_metric"]) as d:
-        assert d.rpc({"fn": "setPerfMonitor"})["status"].startswith("unavailable: ")
+        deadline = time.time() + 10
+        while (st := d.rpc({"fn": "setPerfMonitor"})["status"]) == "starting" and time.time() < deadline:
+            time.sleep(0.05)
+        assert st.startswith("unavailable: ") and "no_such_metric: unknown metric id" in st, st
     with DaemonProcess([]) as d:
         assert d.rpc({"fn": "setPerfMonitor", "enable": True})["status"] == \
             "unavailable: perf monitor not enabled"
+
+
+def test_set_perf_monitor_starting_state_before_counters_open(native_built):
+    """The RPC server serves before the perf monitor has opened its counters
+    (system-wide groups on hundreds of CPUs take a while; here a testing delay
+    stands in for that).  An early setPerfMonitor must answer "starting", not
+    "unavailable: perf monitor not enabled", and the co-sampler must wait it
+    out instead of killing the daemon and falling back."""
+    args = ["--perf_monitor_start_delay_ms=1500", "--perf_monitor_metrics=cpu_clock"]
+    with DaemonProcess(["--enable_perf_monitor", f"--perf_monitor_pids={os.getpid()}", *args]) as d:
+        assert d.rpc({"fn": "setPerfMonitor"})["status"] == "starting"
+        deadline = time.time() + 15
+        while (st := d.rpc({"fn": "setPerfMonitor"}))["status"] == "starting" and time.time() < deadline:
+            time.sleep(0.05)
+        assert st["status"] == "ok" or (st["status"].startswith("unavailable: ") and
+                                        "not enabled" not in st["status"]), st
+    from dynolog_amd.utils.host_pmu import HostPmuCosampler
+    s = HostPmuCosampler("cpu_clock", extra_args=args).start([os.getpid()])
+    try:
+        assert s.running or "not enabled" not in s.reason, s.reason
+        assert s.running == (st["status"] == "ok")
+    finally:
+        s.stop()
 
 
 def test_host_pmu_cosampler_summary(native_built):

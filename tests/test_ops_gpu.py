@@ -195,6 +195,33 @@ def test_fused_adamw_tracks_torch_fused(ops):
         assert diff <= 2e-2, diff
 
 
+def test_fused_adamw_per_param_step_counts(ops):
+    """A param whose grad first appears at step 3 gets step-1 bias correction
+    (per-param step counts, like torch.optim.AdamW), not the group's count."""
+    from dynolog_amd.ops.optim import FusedAdamW
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    base = [torch.randn(s, device=DEV, generator=g).bfloat16() for s in [(256, 64), (1000,)]]
+    pa = [torch.nn.Parameter(b.clone()) for b in base]
+    pb = [torch.nn.Parameter(b.clone()) for b in base]
+    hp = dict(lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    oa = FusedAdamW(pa, **hp)
+    ob = torch.optim.AdamW(pb, fused=True, **hp)
+    for step in range(1, 6):
+        for i, (a, b) in enumerate(zip(pa, pb)):
+            if i == 1 and step < 3:
+                a.grad = b.grad = None  # late grad: skipped by both optimizers
+                continue
+            gr = torch.randn(a.shape, device=DEV, generator=g).bfloat16()
+            a.grad, b.grad = gr.clone(), gr.clone()
+        oa.step()
+        ob.step()
+    assert oa.state[pa[0]]["step"] == 5 and oa.state[pa[1]]["step"] == 3
+    for a, b in zip(pa, pb):
+        diff = (a.float() - b.float()).abs().max().item()
+        assert diff <= 2e-2, diff
+
+
 @pytest.mark.parametrize("R,C", [(8192, 4096), (136, 72), (64, 8)])
 def test_transpose2d(ops, R, C):
     x = torch.randn(R, C, device=DEV).bfloat16()
