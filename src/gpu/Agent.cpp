@@ -338,6 +338,9 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   stopFlag_ = false;
   paused_ = false;
   running_ = true;
+  // set here, not in the sampler thread: a set_rate() right after start
+  // must not be overwritten when the thread comes up
+  setSampleHz(cfg_.sampleHz);
   samplerThread_ = std::thread([this] { samplerLoop(); });
   if (root) consumerThread_ = std::thread([this] { consumerLoop(); });
   // Keep the sampler (and drain consumer) on CPUs NUMA-local to this GPU: its
@@ -413,7 +416,6 @@ bool Agent::flushBatch(int nstaged, std::string* err) {
 
 void Agent::samplerLoop() {
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
-  periodNs_ = static_cast<uint64_t>(1e9 / std::max(1.0, cfg_.sampleHz));
   uint64_t next = monoNs();
   int staged = 0;
   std::string err;
