@@ -12,6 +12,11 @@
 //     uclk_mhz, temperature_hotspot/mem, vram_used_bytes/vram_total_bytes,
 //     xgmi_{rx,tx}_bytes_link<k>, ppt_violation_pct, thermal_violation_pct,
 //     throttle_status, xgmi_hive_id
+//   health (rocm_smi RAS / PCIe / xGMI; the reference only had dcgm_error):
+//     ecc_{correctable,uncorrectable}_total (since driver load) and per-interval
+//     ecc_{correctable,uncorrectable}, ecc_uncorrectable_<block>,
+//     pcie_replay_count / pcie_replays, xgmi_error_status, and the summary
+//     gpu_health (0 ok, 1 degraded, 2 failing) with health_reasons
 // Sampling is a single rsmi_dev_gpu_metrics_info_get() per GPU (~230 us,
 // measured in profiles/round1/probe_counters_inproc.log) plus two sysfs reads.
 #pragma once
@@ -46,7 +51,29 @@ struct SmiSample {
   uint32_t renderMinor = 0;
   uint64_t hiveId = 0;
   std::vector<uint32_t> pids;        // compute processes on this GPU
+  // health: cumulative RAS error counts per GPU block (index = bit of
+  // rsmi_gpu_block_t), PCIe replay counter, xGMI error status (-1 unknown)
+  static constexpr int kEccBlocks = 14;
+  bool eccValid = false;
+  uint64_t eccCorr[kEccBlocks] = {}, eccUncorr[kEccBlocks] = {};
+  bool pcieReplayValid = false;
+  uint64_t pcieReplay = 0;
+  int xgmiErrStatus = -1;
 };
+
+// Short lower-case name of RAS block `bit` ("umc", "sdma", "gfx", ...).
+const char* eccBlockName(int bit);
+
+struct GpuHealth {
+  int level = 0;  // 0 ok, 1 degraded, 2 failing
+  std::string reasons;  // '+'-joined, empty when ok
+};
+
+// Health of one GPU from its previous and current sample: failing on a read
+// failure, new uncorrectable ECC errors or an xGMI link error; degraded on new
+// correctable errors, new PCIe replays, or thermal / power throttling for
+// more than half of the interval.
+GpuHealth evaluateGpuHealth(const SmiSample* prev, const SmiSample& cur);
 
 // Emits the record for one GPU given the previous and current sample.
 void logSmiRecord(Logger& log, int device, const SmiSample* prev, const SmiSample& cur,
@@ -71,7 +98,10 @@ class SmiMonitor {
 
  private:
   bool readDevice(int dev, SmiSample* out);
+  void readHealth(int dev, SmiSample* out);
   int numDevices_ = 0;
+  std::vector<uint64_t> eccMask_;        // per device: RAS blocks still queried
+  std::map<int, uint64_t> injectedUc_;   // --fault_inject=ecc_uc
   SampleFn sampleFn_;
   std::vector<SmiSample> prev_, cur_;
   std::vector<std::map<std::string, std::string>> attribution_;

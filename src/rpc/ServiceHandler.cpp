@@ -1,5 +1,8 @@
 #include "rpc/ServiceHandler.h"
 
+#include <algorithm>
+#include <map>
+
 #include "common/Flags.h"
 #include "common/Logging.h"
 #include "sinks/MetricStore.h"
@@ -43,6 +46,33 @@ Json ServiceHandler::listCollectors() {
   Json j = Json::object();
   j["collectors"] = store_ ? Json(store_->collectors()) : Json::array();
   return j;
+}
+
+Json gpuHealthSummary(const Json& records) {
+  // latest record per device (records are oldest first)
+  std::map<int64_t, const Json*> latest;
+  if (records.isArray())
+    for (const auto& r : records.asArray())
+      if (r.isObject() && r.contains("device") && r.contains("gpu_health")) latest[r.at("device").asInt()] = &r;
+  Json out = Json::object();
+  Json devs = Json::array();
+  int64_t worst = latest.empty() ? -1 : 0;
+  for (const auto& [dev, r] : latest) {
+    Json d = Json::object();
+    for (const char* k : {"device", "gpu_health", "health_reasons", "smi_error", "ecc_correctable_total",
+                          "ecc_uncorrectable_total", "ecc_correctable", "ecc_uncorrectable",
+                          "pcie_replay_count", "pcie_replays", "xgmi_error_status", "temperature_hotspot",
+                          "temperature_mem", "thermal_violation_pct", "ppt_violation_pct",
+                          "throttle_status"})
+      if (r->contains(k)) d[k] = r->at(k);
+    worst = std::max<int64_t>(worst, r->at("gpu_health").asInt());
+    devs.push_back(d);
+  }
+  out["num_gpus"] = static_cast<int64_t>(latest.size());
+  out["worst"] = worst;
+  out["devices"] = devs;
+  if (latest.empty()) out["status"] = "no GPU records yet (daemon needs --enable_gpu_monitor)";
+  return out;
 }
 
 std::shared_ptr<RpcDispatcher> makeDispatcher(std::shared_ptr<ServiceHandler> h) {
@@ -104,6 +134,11 @@ std::shared_ptr<RpcDispatcher> makeDispatcher(std::shared_ptr<ServiceHandler> h)
                                : "";
     return h->store()->stats(c, req.at("key").asString(), windowMs, fk,
                              req.contains("filter_value") ? req.at("filter_value") : Json());
+  });
+  // {"fn":"getGpuHealth"}: per GPU, the latest health summary of the
+  // rocm_smi monitor (gpu_health 0 ok / 1 degraded / 2 failing + reasons)
+  d->add("getGpuHealth", [h](const Json&) -> std::optional<Json> {
+    return gpuHealthSummary(h->store() ? h->store()->last("gpu", 256) : Json::array());
   });
   d->add("getMetrics", [h](const Json& req) -> std::optional<Json> {
     try {

@@ -51,8 +51,24 @@ def test_smi_gpu_monitor(native_built):
         assert r["device"] >= 0
         assert int(r["vram_total_bytes"]) > 200 * 2**30  # 288 GB HBM3E
         for k in ("gfx_activity", "umc_activity", "socket_power", "gpu_device_utilization",
-                  "gpu_power_draw", "gpu_frequency_mhz", "temperature_hotspot"):
+                  "gpu_power_draw", "gpu_frequency_mhz", "temperature_hotspot", "gpu_health"):
             assert k in r, k
+        # a healthy box: no failing GPU (RAS counts may be unreadable as non-root)
+        assert r["gpu_health"] in (0, 1), r
+
+
+def test_smi_gpu_health_fault_injection(native_built):
+    """--fault_inject=ecc_uc adds one uncorrectable UMC error per tick: the
+    record reports it per interval and the GPU as failing."""
+    with DaemonProcess(["--enable_gpu_monitor", "--gpu_monitor_reporting_interval_ms=300",
+                        "--fault_inject=ecc_uc"]) as d:
+        recs = _wait_records(d, "gpu", lambda r: r.get("ecc_uncorrectable", 0) >= 1)
+        bad = [r for r in recs if r.get("ecc_uncorrectable", 0) >= 1]
+        assert bad, d.log()[-3000:]
+        r = bad[-1]
+        assert r["gpu_health"] == 2, r
+        assert "ecc_uncorrectable" in r["health_reasons"], r
+        assert int(r["ecc_uncorrectable_umc"]) >= 1, r
 
 
 def test_out_of_process_device_counters(native_built):
