@@ -650,6 +650,33 @@ void Agent::setPhaseName(uint32_t id, const std::string& name) {
   agg_.setPhaseName(id, name);
 }
 
+std::vector<Json> Agent::counterTrackEvents(uint64_t t0, uint64_t t1) const {
+  std::lock_guard<std::mutex> lk(aggMu_);
+  return agg_.counterTrackEvents(t0, t1, static_cast<int>(getpid()));
+}
+
+bool Agent::writeKernelTrace(const std::string& path, std::string* err) const {
+  auto& kt = KernelTracer::get();
+  std::vector<Json> tracks;
+  if (running_) {
+    const auto [t0, t1] = kt.window();
+    // the window's last samples reach rank 0 with the next step()'s gather:
+    // give the training loop up to 1 s to deliver them
+    const uint64_t deadline = monoNs() + 1000000000ull;
+    while (cfg_.rank == 0 && !paused_ && monoNs() < deadline) {
+      {
+        std::lock_guard<std::mutex> lk(aggMu_);
+        uint64_t oldest = UINT64_MAX;
+        for (int r = 0; r < agg_.world(); ++r) oldest = std::min(oldest, agg_.rank(r).last.host_ts_ns);
+        if (oldest >= t1) break;
+      }
+      usleep(20000);
+    }
+    tracks = counterTrackEvents(t0, t1);
+  }
+  return kt.writeChromeTrace(path, err, &tracks);
+}
+
 Json Agent::phaseStats() const {
   std::lock_guard<std::mutex> lk(aggMu_);
   return agg_.phaseStats();
@@ -718,7 +745,9 @@ void Agent::controlLoop() {
         res["summary"] = kt.summary(static_cast<size_t>(std::max(top, 1)));
         if (req.contains("chrome_path") && req.at("chrome_path").isString()) {
           const std::string path = req.at("chrome_path").asString();
-          if (kt.writeChromeTrace(path, &err)) res["chrome_path"] = path;
+          // flush pending samples so the counter tracks cover the window
+          if (cfg_.rank == 0 && !paused_) packPending();
+          if (writeKernelTrace(path, &err)) res["chrome_path"] = path;
           else res["chrome_error"] = err;
         }
       }

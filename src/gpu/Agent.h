@@ -92,6 +92,11 @@ class Agent {
   bool mark(uint32_t phase, hipStream_t stream, std::string* err);
   void setPhaseName(uint32_t id, const std::string& name);
   Json phaseStats() const;
+  // Counter-track trace events of the samples in [t0, t1] (rank 0 sees every
+  // rank's; other ranks have none) for KernelTracer::writeChromeTrace.
+  std::vector<Json> counterTrackEvents(uint64_t t0, uint64_t t1) const;
+  // Kernel trace Chrome JSON with this agent's counter tracks under it.
+  bool writeKernelTrace(const std::string& path, std::string* err) const;
   void stop();
   bool running() const { return running_; }
 

@@ -246,8 +246,14 @@ Json KernelTracer::summary(size_t topN) const {
   return j;
 }
 
-bool KernelTracer::writeChromeTrace(const std::string& path, std::string* err) const {
-  std::vector<KernelRecord> recs = records();
+std::pair<uint64_t, uint64_t> KernelTracer::window() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return {windowStart_, active_ ? monoNow() : windowEnd_};
+}
+
+bool KernelTracer::writeChromeTrace(const std::string& path, std::string* err,
+                                    const std::vector<Json>* extra) const {
+  std::vector<KernelRecord> recs = records();  // already on CLOCK_MONOTONIC (bufferCb)
   std::ofstream f(path);
   if (!f) {
     if (err) *err = "cannot write " + path;
@@ -276,6 +282,11 @@ bool KernelTracer::writeChromeTrace(const std::string& path, std::string* err) c
     f << (first ? "" : ",\n") << e.dump();
     first = false;
   }
+  if (extra)
+    for (const auto& e : *extra) {
+      f << (first ? "" : ",\n") << e.dump();
+      first = false;
+    }
   f << "\n],\"displayTimeUnit\":\"ms\",\"otherData\":{\"clock\":\"CLOCK_MONOTONIC\",\"source\":\"dynolog-amd agent\"}}\n";
   return static_cast<bool>(f);
 }

@@ -58,8 +58,13 @@ class KernelTracer {
   std::string kernelName(uint64_t kernelId) const;
   // Per-kernel totals ranked by GPU time, busy fraction of the window.
   Json summary(size_t topN = 20) const;
-  // Chrome trace-event JSON (chrome://tracing, Perfetto).
-  bool writeChromeTrace(const std::string& path, std::string* err) const;
+  // Chrome trace-event JSON (chrome://tracing, Perfetto), timestamps on
+  // CLOCK_MONOTONIC; `extra` events (e.g. the agent's counter tracks) are
+  // appended as given.
+  bool writeChromeTrace(const std::string& path, std::string* err,
+                        const std::vector<Json>* extra = nullptr) const;
+  // Last trace window, CLOCK_MONOTONIC ns (end = now while tracing).
+  std::pair<uint64_t, uint64_t> window() const;
   // Start/End tag-stack events per dispatch (tag = kernel id, compUnit = GPU).
   std::vector<tagstack::Event> events() const;
 

@@ -139,6 +139,48 @@ def test_kernel_trace_in_process(native_built, tmp_path):
     assert gpu0 and sum(gpu0.values()) > 0
 
 
+def test_kernel_trace_with_counter_tracks(native_built, tmp_path):
+    """With the agent sampling, the kernel trace's Chrome JSON carries the
+    1 kHz counters as counter tracks ("ph": "C") on the same clock as the
+    dispatches, and the GEMM-heavy window shows MFMA activity."""
+    chrome = str(tmp_path / "kernels_counters.json")
+    res = _run(f"""
+        from dynolog_amd import agent
+        agent.preinit(kernel_trace=True)
+        import json, time, torch
+        ag = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
+        x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+        y = x @ x; torch.cuda.synchronize()
+        with agent.KernelTrace() as kt:
+            t0 = time.time()
+            while time.time() - t0 < 0.3:
+                for _ in range(4):
+                    y = x @ x
+                ag.step()
+                torch.cuda.synchronize()
+        ag.pack_pending(); ag.step(); torch.cuda.synchronize(); ag.flush()
+        kt.write_chrome({chrome!r})
+        ag.stop()
+        print("RESULT " + json.dumps(dict(ok=True)))
+    """)
+    assert res["ok"]
+    with open(chrome) as f:
+        evs = json.load(f)["traceEvents"]
+    kern = [e for e in evs if e["ph"] == "X"]
+    ctr = [e for e in evs if e["ph"] == "C"]
+    assert kern and ctr, (len(kern), len(ctr))
+    names = {e["name"] for e in ctr}
+    assert {"gpu0 mfma_util_pct", "gpu0 hbm_gbps", "gpu0 bf16_tflops"} <= names, names
+    k0 = min(e["ts"] for e in kern)
+    k1 = max(e["ts"] + e["dur"] for e in kern)
+    ts = [e["ts"] for e in ctr]
+    # same clock: the samples fall inside the traced window (+/- 50 ms)
+    assert k0 - 50e3 <= min(ts) and max(ts) <= k1 + 50e3, (k0, k1, min(ts), max(ts))
+    mfma = [e["args"]["mfma_util"] for e in ctr if e["name"] == "gpu0 mfma_util_pct"]
+    assert len(mfma) >= 100, len(mfma)           # ~300 samples at 1 kHz over 0.3 s
+    assert max(mfma) > 10.0, max(mfma)
+
+
 def test_phase_markers_attribute_samples(native_built):
     """GPU-stream phase markers: samples taken while the GPU runs the GEMM
     phase show MFMA work, samples in the copy phase show HBM traffic."""
