@@ -497,10 +497,12 @@ void Agent::samplerLoop() {
     if (now < next) {
       timespec ts{static_cast<time_t>(next / 1000000000ull), static_cast<long>(next % 1000000000ull)};
       clock_nanosleep(CLOCK_MONOTONIC, TIMER_ABSTIME, &ts, nullptr);
-    } else {
-      if (now - next > period) lateTicks_++;
-      next = now;  // behind schedule: do not burst to catch up
+    } else if (now - next > period) {
+      lateTicks_++;
+      next = now;  // more than a tick behind: drop the missed ticks, do not burst
     }
+    // less than a tick behind (one slow sample): sample again right away and
+    // keep the schedule's phase, so the achieved rate stays at the target
   }
   if (staged > 0 && flushBatch(staged, &err)) staged = 0;
   hipWarn(hipStreamSynchronize(packStream_), "pack stream sync");
