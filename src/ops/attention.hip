@@ -507,20 +507,26 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv8_kernel(
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
         }
         const int key = kw0 + col;
+        auto softmax_grad = [&](auto diagc) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 L = *reinterpret_cast<const float4*>(lsel + 32 * qh + 8 * g + 4 * h);
-          const float4 Dl = *reinterpret_cast<const float4*>(dell + 32 * qh + 8 * g + 4 * h);
-          const float Lv[4] = {L.x, L.y, L.z, L.w}, Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
+          for (int g = 0; g < 4; ++g) {
+            const float4 L = *reinterpret_cast<const float4*>(lsel + 32 * qh + 8 * g + 4 * h);
+            const float4 Dl = *reinterpret_cast<const float4*>(dell + 32 * qh + 8 * g + 4 * h);
+            const float Lv[4] = {L.x, L.y, L.z, L.w}, Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i;
-            float p = ex2(sa[r] * c - Lv[i]);
-            if (diag && key > qs0 + 8 * g + 4 * h + i) p = 0.f;
-            pa[r] = p * (pa[r] - Dv[i]);
-            sa[r] = p;
+            for (int i = 0; i < 4; ++i) {
+              const int r = 4 * g + i;
+              float p = ex2(sa[r] * c - Lv[i]);
+              if constexpr (decltype(diagc)::value)
+                if (key > qs0 + 8 * g + 4 * h + i) p = 0.f;
+              pa[r] = p * (pa[r] - Dv[i]);
+              sa[r] = p;
+            }
           }
-        }
+        };
+        // wave-uniform: only the diagonal sub-tiles pay for the mask
+        if (diag) softmax_grad(std::true_type{});
+        else softmax_grad(std::false_type{});
         const bf16x8 pb[2] = {acc_operand(sa, 0), acc_operand(sa, 1)};
         const bf16x8 zb[2] = {acc_operand(pa, 0), acc_operand(pa, 1)};
 #pragma unroll
@@ -648,12 +654,17 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(
         for (int s = 0; s < 8; ++s) pacc = mfma(fr[s], df[s], pacc);
         __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        if (diag) {  // wave-uniform: only the tiles on this wave's diagonal pay for the mask
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = k0 + 32 * half + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float x = ex2(sacc[r] * c - L);
-          if (diag && key > qrow) x = 0.f;
-          sacc[r] = x * (pacc[r] - Dl);
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + 32 * half + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float x = ex2(sacc[r] * c - L);
+            if (key > qrow) x = 0.f;
+            sacc[r] = x * (pacc[r] - Dl);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[r] = ex2(sacc[r] * c - L) * (pacc[r] - Dl);
         }
         z[half] = sacc;
       }
