@@ -176,6 +176,11 @@ class GpuAgent:
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
 
+        ``gather_mode``: "gather" (ncclGather to rank 0 over xGMI, default),
+        "allgather", "shm" (one node: ranks > 0 publish into a shared-memory
+        mailbox rank 0 drains; no second communicator, works with several
+        ranks on one GPU) or "none" (each rank keeps its samples).
+
         ``sinks``: any of "json" (daemon-format log lines), "memory" (queryable
         via memory_records()), "prometheus", "daemon" (forward every per-GPU
         record to the node's dynolog daemon over the IPC fabric as a "gmet"
@@ -184,8 +189,13 @@ class GpuAgent:
             raise AgentError("dynolog_amd.agent.preinit() must be called before HIP init")
         lib = _native.load_gpu_lib()
         if world > 1 and gather_mode != "none" and uid is None:
+            # RCCL modes: the communicator's unique id; "shm": a random tag that
+            # names the node-local mailbox segment
             import torch.distributed as dist
-            obj = [nccl_unique_id() if rank == 0 else None]
+            mine = None
+            if rank == 0:
+                mine = os.urandom(16) if gather_mode == "shm" else nccl_unique_id()
+            obj = [mine]
             dist.broadcast_object_list(obj, src=0, group=process_group)
             uid = obj[0]
         cfg = dict(device=device, rank=rank, world=world, sample_hz=sample_hz, batch=batch,
