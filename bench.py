@@ -33,6 +33,20 @@ METRIC = "counter samples/sec/GPU + tracing overhead % on Llama-3-8B train, 1/2/
 # Reference effective GPU counter rate: DCGM watch every 10 s = 0.1 samples/s/GPU
 # (BASELINE.md row "GPU metric sampling interval (DCGM)", dynolog/src/Main.cpp:42-45).
 BASELINE_SAMPLES_PER_SEC_PER_GPU = 0.1
+# MI355X dense bf16 MFMA peak (no sparsity), for the MFU field
+PEAK_BF16_FLOPS = 2.5e15
+
+
+def model_flops_per_step(cfg, batch: int, seq: int) -> float:
+    """FLOPs of one training step on one GPU: 6 x (matmul parameters) x tokens
+    plus causal attention, 2 products forward and 5 backward (the standard
+    flash-attention count; the kernels' recompute is not credited)."""
+    d, f, L, hd = cfg.d_model, cfg.ffn_dim, cfg.n_layers, cfg.head_dim
+    kv = cfg.n_kv_heads * hd
+    matmul_params = L * (d * (d + 2 * kv) + d * d + 3 * d * f) + cfg.vocab_size * d
+    tokens = batch * seq
+    attn_fwd = 2 * 2 * batch * cfg.n_heads * seq * seq * hd / 2 * L  # QK^T + PV, causal half
+    return 6.0 * matmul_params * tokens + attn_fwd * (1.0 + 2.5)
 
 
 def parse_args(argv=None):
@@ -292,6 +306,11 @@ def main(argv=None) -> int:
             "overhead_pct_headline_window": round((meas_s / base_s - 1.0) * 100.0, 3) if base_s else None,
             "ab_windows": {"steps": args.ab_steps, "rounds": args.ab_rounds} if base_s else None,
             "tokens_per_sec": round(tokens / meas_s, 1),
+            # model FLOPs actually computed per GPU: 6 x matmul params x tokens
+            # (fwd + dgrad + wgrad) + causal attention (QK^T, PV fwd; 5 bwd
+            # products with the dQ-kernel recompute counted as in the kernels)
+            "model_tflops_per_gpu": round(model_flops_per_step(cfg, B, S) * args.steps / meas_s * 1e-12, 1),
+            "mfu_pct": round(100.0 * model_flops_per_step(cfg, B, S) * args.steps / meas_s / PEAK_BF16_FLOPS, 2),
             "loss": round(loss_val, 4),
             "vs_baseline_note": "value / (0.1 samples/s/GPU x n_gpus): reference DCGM 10 s interval",
         }
