@@ -189,6 +189,7 @@ struct Stage {
 // running max moved (exact); half of the V^T fragments read right after the
 // S MFMAs so their LDS latency hides under the softmax (r75, +3.5 %).
 constexpr int FQ = 256, FK = 64, FW = 8, FSTAGES = 4;
+constexpr float kDeferMax = 8.0f;
 constexpr int FTILE = FK * ROWB;  // one K or V tile image, 16 KiB
 constexpr int FNT = 64 * FW;
 
@@ -266,8 +267,12 @@ __device__ __forceinline__ void fwd_tile(const unsigned char* kt, const unsigned
     }
     mb = max3(mb, s1[r], s1[r + 1]);
   }
-  const float mt = fmaxf(ma, mb);
-  const float mn = fmaxf(m, pair_max(mt) * c);  // finite: key tile 0 always has an unmasked key
+  const float mt = pair_max(fmaxf(ma, mb)) * c;
+  // Deferred max: the running max only moves when the tile's max exceeds it
+  // by more than kDeferMax (log2 units), so p = exp2(c*s - m) stays <= 2^8
+  // and most tiles skip the O rescale below (alpha == 1 in every lane).  The
+  // first tile always sets m (m starts at -inf; key tile 0 has an unmasked key).
+  const float mn = mt > m + kDeferMax ? mt : m;
   const float alpha = ex2(m - mn);
   m = mn;
   float rs = 0.f;
