@@ -188,6 +188,19 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     log::setSink([f](log::Severity, const std::string& l) { *f << l << "\n" << std::flush; });
   }
   HIP_OK(hipSetDevice(cfg_.device), "hipSetDevice");
+  // leftovers of an earlier start() that failed part-way (the caller may
+  // retry with another gather mode, agent.py)
+  if (sampler_) sampler_->stop();
+  if (comm_) {
+    ncclCommDestroy(comm_);
+    comm_ = nullptr;
+  }
+  if (shm_) {
+    if (shmDev_) hipWarn(hipHostUnregister(shm_->base()), "hipHostUnregister mailbox");
+    shmDev_ = nullptr;
+    shm_.reset();
+  }
+  releaseDevice();
 
   // map HIP device -> rocprofiler agent by PCI location
   int agentIdx = cfg_.agentIndex;
@@ -875,9 +888,57 @@ void Agent::stop() {
     shmDev_ = nullptr;
     shm_.reset();  // rank 0 unlinks the segment
   }
+  releaseDevice();
   running_ = false;
   LOG(INFO) << "GPU agent stopped: " << samplesTaken_.load() << " samples, " << batches_.load()
             << " batches, " << gathers_.load() << " gathers";
+}
+
+// Per-start device state: the ring (2^20 slots ~ 400 MB of HBM by default),
+// staging, gather buffers, events and streams.  Freed at stop() and before a
+// (re)start, so a failed start followed by a fallback start, or repeated
+// start/stop in one process, does not accumulate HBM.  The pinned staging
+// buffers (hStage_) are kept and reused across starts.
+void Agent::releaseDevice() {
+  auto freeDev = [](auto*& p) {
+    if (p) hipWarn(hipFree(p), "hipFree");
+    p = nullptr;
+  };
+  auto freeHost = [](auto*& p) {
+    if (p) hipWarn(hipHostFree(p), "hipHostFree");
+    p = nullptr;
+  };
+  auto destroyEvent = [](hipEvent_t& e) {
+    if (e) hipWarn(hipEventDestroy(e), "hipEventDestroy");
+    e = nullptr;
+  };
+  if (dHdr_) hipWarn(hipFree(dHdr_), "hipFree ring");
+  dHdr_ = nullptr;
+  dRing_ = nullptr;
+  freeDev(dStage_);
+  freeDev(dMeta_);
+  for (auto& c : dCarry_) freeDev(c);
+  freeDev(dPerm_);
+  freeDev(dSegStart_);
+  freeDev(dSegLen_);
+  freeDev(dSend_);
+  for (int i = 0; i < kRecv; ++i) {
+    freeDev(dRecv_[i]);
+    freeHost(hRecv_[i]);
+    destroyEvent(gathered_[i]);
+    destroyEvent(drained_[i]);
+    recvUsed_[i] = false;
+  }
+  recvNext_ = 0;
+  {
+    std::lock_guard<std::mutex> g(packMu_);
+    for (auto& e : packEvents_) destroyEvent(e);
+    lastPack_ = nullptr;
+  }
+  freeHost(hPhase_);
+  if (packStream_) hipWarn(hipStreamDestroy(packStream_), "hipStreamDestroy pack");
+  if (drainStream_) hipWarn(hipStreamDestroy(drainStream_), "hipStreamDestroy drain");
+  packStream_ = drainStream_ = nullptr;
 }
 
 Json Agent::stats() const {

@@ -116,6 +116,7 @@ class Agent {
   void consumerLoop();
   void logInterval();
   bool setupLayout(const std::vector<uint64_t>& ids, std::string* err);
+  void releaseDevice();
   std::unique_ptr<Logger> makeLogger();
 
   AgentConfig cfg_;

@@ -321,3 +321,31 @@ def test_rccl_gather_path_with_one_rank(native_built, mode):
     assert st["last_error"] == "" and not st["gather_failed"], st
     assert st["gathers"] >= 40, st
     assert res["wc"][0] > 0 and st["ranks"][0]["received"] >= res["wc"][0], st
+
+
+def test_agent_restart_returns_device_memory(native_built):
+    """stop() frees the per-start device state (the 2^20-slot HBM ring,
+    staging, gather buffers, streams): five start/stop cycles in one process
+    leave device memory where one cycle left it, and every restart samples."""
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit()
+        import json, time, torch
+        torch.cuda.set_device(0)
+        torch.zeros(1, device="cuda")
+        free = []
+        taken = []
+        for i in range(5):
+            a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
+            time.sleep(0.2)
+            a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+            taken.append(a.stats()["samples_taken"])
+            a.stop()
+            torch.cuda.synchronize()
+            free.append(torch.cuda.mem_get_info()[0])
+        print("RESULT " + json.dumps(dict(free=free, taken=taken)))
+    """)
+    free = res["free"]
+    assert all(t > 50 for t in res["taken"]), res["taken"]
+    # the ring alone is ~400 MB; allow allocator noise well below one ring
+    assert free[0] - min(free[1:]) < 64 << 20, free
