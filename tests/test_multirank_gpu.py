@@ -31,7 +31,7 @@ def test_two_rank_ddp_bench_rehearsal(native_built):
     assert out["agent"]["samples_taken"] > 0 and out["agent"]["samples_failed"] == 0
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_shm_gather_multirank_bench_rehearsal(native_built, world):
     """--gather-mode shm: every rank's counter slots reach rank 0 through the
     node-local mailbox, so the multi-rank aggregation (per-rank window counts,
