@@ -40,20 +40,26 @@ class SharedCounters:
             self.names.append(raw.split(b"\0", 1)[0].decode())
         self._base: Optional[Dict[str, float]] = None
 
-    def snapshot(self, retries: int = 1000) -> dict:
-        """Consistent per-CPU snapshot (seqlock read)."""
+    def snapshot(self, timeout_s: float = 2.0) -> dict:
+        """Consistent per-CPU snapshot (seqlock read).  Retries while the
+        writer holds the sequence odd or moved it under the read; a writer
+        descheduled mid-update (loaded host) can hold it for a scheduler
+        tick, so the bound is time, not a retry count."""
         row = struct.Struct("=" + "d" * (self.num_events + 2))
-        for _ in range(retries):
+        deadline = time.monotonic() + timeout_s
+        tries = 0
+        while True:
             seq0 = struct.unpack_from("=Q", self._mm, 24)[0]
-            if seq0 & 1:
-                time.sleep(0)
-                continue
-            _, _, _, _, _, _, update_ns, publishes = _HDR.unpack_from(self._mm, 0)
-            per_cpu = [list(row.unpack_from(self._mm, _DATA_OFF + c * row.size))[:self.num_events]
-                       for c in range(self.num_cpus)]
-            if struct.unpack_from("=Q", self._mm, 24)[0] == seq0:
-                return {"update_ns": update_ns, "publishes": publishes, "per_cpu": per_cpu}
-        raise TimeoutError("shared counters: writer kept the seqlock busy")
+            if not seq0 & 1:
+                _, _, _, _, _, _, update_ns, publishes = _HDR.unpack_from(self._mm, 0)
+                per_cpu = [list(row.unpack_from(self._mm, _DATA_OFF + c * row.size))[:self.num_events]
+                           for c in range(self.num_cpus)]
+                if struct.unpack_from("=Q", self._mm, 24)[0] == seq0:
+                    return {"update_ns": update_ns, "publishes": publishes, "per_cpu": per_cpu}
+            tries += 1
+            if time.monotonic() > deadline:
+                raise TimeoutError("shared counters: writer kept the seqlock busy")
+            time.sleep(0 if tries < 100 else 0.0005)
 
     def totals(self) -> Dict[str, float]:
         snap = self.snapshot()

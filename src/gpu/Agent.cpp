@@ -777,8 +777,22 @@ bool Agent::writeKernelTrace(const std::string& path, std::string* err) const {
       usleep(20000);
     }
     tracks = counterTrackEvents(t0, t1);
+    if (!tracks.empty()) {
+      Json m = Json::object();
+      m["name"] = "process_name";
+      m["ph"] = "M";
+      m["ts"] = 0;
+      m["pid"] = static_cast<int>(getpid());
+      m["tid"] = 0;
+      m["args"] = Json::object();
+      m["args"]["name"] = "dynolog-amd counters (" + std::to_string(agg_.world()) + " rank(s), 1 kHz)";
+      tracks.push_back(m);
+    }
   }
-  return kt.writeChromeTrace(path, err, &tracks);
+  TraceMeta meta;
+  meta.rank = cfg_.rank;
+  meta.world = cfg_.world;
+  return kt.writeChromeTrace(path, err, &tracks, &meta);
 }
 
 Json Agent::phaseStats() const {

@@ -40,6 +40,17 @@ struct KernelRecord {
   uint32_t ldsBytes = 0, scratchBytes = 0;
 };
 
+// Per kernel symbol: register budget from the code object (occupancy args).
+struct KernelSymbol {
+  std::string name;
+  uint32_t archVgpr = 0, accumVgpr = 0, sgpr = 0;
+};
+
+// Trace-wide metadata for the Kineto-layout header (distributedInfo).
+struct TraceMeta {
+  int rank = -1, world = 0;
+};
+
 class KernelTracer {
  public:
   static KernelTracer& get();
@@ -58,18 +69,23 @@ class KernelTracer {
   std::string kernelName(uint64_t kernelId) const;
   // Per-kernel totals ranked by GPU time, busy fraction of the window.
   Json summary(size_t topN = 20) const;
-  // Chrome trace-event JSON (chrome://tracing, Perfetto), timestamps on
-  // CLOCK_MONOTONIC; `extra` events (e.g. the agent's counter tracks) are
-  // appended as given.
+  // Chrome trace-event JSON in libkineto's layout (schemaVersion,
+  // deviceProperties, distributedInfo; GPU events with pid = device, tid =
+  // stream, args device / stream / correlation / grid / block / registers per
+  // thread / shared memory / est. occupancy), so Perfetto, chrome://tracing,
+  // TensorBoard's profiler and Holistic Trace Analysis read it like a PyTorch
+  // profiler trace.  Timestamps are CLOCK_MONOTONIC us; `extra` events (the
+  // agent's counter tracks) are appended as given.
   bool writeChromeTrace(const std::string& path, std::string* err,
-                        const std::vector<Json>* extra = nullptr) const;
+                        const std::vector<Json>* extra = nullptr, const TraceMeta* meta = nullptr) const;
+  Json traceDocument(const std::vector<Json>* extra, const TraceMeta* meta) const;
   // Last trace window, CLOCK_MONOTONIC ns (end = now while tracing).
   std::pair<uint64_t, uint64_t> window() const;
   // Start/End tag-stack events per dispatch (tag = kernel id, compUnit = GPU).
   std::vector<tagstack::Event> events() const;
 
   // --- rocprofiler callbacks ---
-  void onKernelSymbol(uint64_t kernelId, const char* name);
+  void onKernelSymbol(uint64_t kernelId, const KernelSymbol& sym);
   void onRecords(const KernelRecord* recs, size_t n, uint64_t dropped);
   int64_t clockOffsetNs() const { return clockOffset_; }
 
@@ -78,7 +94,7 @@ class KernelTracer {
   bool configured_ = false;
   bool active_ = false;
   uint64_t codeCtx_ = 0, traceCtx_ = 0, buffer_ = 0;
-  std::map<uint64_t, std::string> names_;
+  std::map<uint64_t, KernelSymbol> names_;
   std::map<uint64_t, int> agentIndex_;
   std::vector<KernelRecord> recs_;
   uint64_t dropped_ = 0;

@@ -169,6 +169,14 @@ int RocprofRuntime::toolInit() {
     ai.domain = a.domain;
     ai.gpu_id = a.gpu_id;
     ai.logical_node_type_id = a.logical_node_type_id;
+    ai.product = a.product_name ? a.product_name : "";
+    ai.lds_kb = a.lds_size_in_kb;
+    ai.wave_size = a.wave_front_size ? a.wave_front_size : 64;
+    ai.max_waves_per_cu = a.max_waves_per_cu;
+    ai.workgroup_max_size = a.workgroup_max_size;
+    ai.gfx_target_version = a.gfx_target_version;
+    ai.max_clock_mhz = a.max_engine_clk_fcompute;
+    ai.local_mem_bytes = a.local_mem_size;
     agents_.push_back(ai);
   }
   for (const auto& ai : agents_) {

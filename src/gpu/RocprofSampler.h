@@ -39,6 +39,11 @@ struct AgentInfo {
   uint32_t location_id = 0, domain = 0;
   uint64_t gpu_id = 0;
   int32_t logical_node_type_id = -1;
+  // for trace headers (Kineto deviceProperties) and occupancy estimates
+  std::string product;
+  uint32_t lds_kb = 0, wave_size = 64, max_waves_per_cu = 0, workgroup_max_size = 0;
+  uint32_t gfx_target_version = 0, max_clock_mhz = 0;
+  uint64_t local_mem_bytes = 0;
 };
 
 // Process-wide registration state.

@@ -132,9 +132,22 @@ def test_kernel_trace_in_process(native_built, tmp_path):
     assert 0 < s["gpu_busy_ms"] <= s["window_ms"] + 1.0
     with open(chrome) as f:
         tr = json.load(f)
-    evs = tr["traceEvents"]
+    evs = [e for e in tr["traceEvents"] if e["ph"] == "X"]
     assert len(evs) == s["dispatches"]
-    assert all(e["ph"] == "X" and e["dur"] >= 0 for e in evs)
+    assert all(e["dur"] >= 0 and e["cat"] == "kernel" for e in evs)
+    # libkineto's trace layout (readable by TensorBoard / Holistic Trace Analysis)
+    assert tr["schemaVersion"] == 1
+    dev = tr["deviceProperties"]
+    assert dev and dev[0]["id"] == 0 and dev[0]["warpSize"] == 64 and dev[0]["numSms"] >= 200, dev
+    for e in evs:
+        a = e["args"]
+        assert e["pid"] == a["device"] == 0 and e["tid"] == a["stream"], e
+        assert len(a["grid"]) == 3 and len(a["block"]) == 3 and "correlation" in a
+        assert a["registers per thread"] > 0 and 0 <= a["est. achieved occupancy %"] <= 100, a
+    gemm = [e for e in evs if "Cijk" in e["name"] or "gemm" in e["name"].lower()]
+    assert gemm and all(e["args"]["grid"][0] * e["args"]["block"][0] > 0 for e in gemm)
+    meta = {(m["name"], m["pid"]) for m in tr["traceEvents"] if m["ph"] == "M"}
+    assert ("process_name", 0) in meta and any(n == "thread_name" for n, _ in meta), meta
     gpu0 = res["slices"].get("gpu0", {})
     assert gpu0 and sum(gpu0.values()) > 0
 
