@@ -200,6 +200,8 @@ def main(argv=None) -> int:
                 torch.cuda.synchronize()
             last_loss[0] = loss
 
+        local_s = [0.0]
+
         def timed(k: int) -> tuple[float, int, int]:
             pdist.barrier()
             torch.cuda.synchronize()
@@ -208,6 +210,7 @@ def main(argv=None) -> int:
             for _ in range(k):
                 train_step()
             torch.cuda.synchronize()
+            local_s[0] = time.perf_counter() - t0  # this rank's own work, before the closing barrier
             pdist.barrier()
             t1 = time.perf_counter()
             m1 = dagent.mono_ns() if ag else 0
@@ -229,6 +232,12 @@ def main(argv=None) -> int:
             torch.cuda.synchronize()
 
         meas_s, m0, m1 = timed(args.steps)
+        # per-rank time to finish its own steps inside the headline window
+        # (stragglers / imbalance show here; the window itself ends at the barrier)
+        rank_local = [local_s[0]]
+        if torch.distributed.is_initialized():
+            rank_local = [None] * env.world
+            torch.distributed.all_gather_object(rank_local, local_s[0])
         loss_val = float(last_loss[0].item()) if torch.is_tensor(last_loss[0]) else last_loss[0]
 
         total_samples = 0
@@ -308,6 +317,7 @@ def main(argv=None) -> int:
             "overhead_pct_headline_window": round((meas_s / base_s - 1.0) * 100.0, 3) if base_s else None,
             "ab_windows": {"steps": args.ab_steps, "rounds": args.ab_rounds} if base_s else None,
             "tokens_per_sec": round(tokens / meas_s, 1),
+            "rank_local_ms_per_step": [round(x / args.steps * 1e3, 3) for x in rank_local],
             # model FLOPs actually computed per GPU: 6 x matmul params x tokens
             # (fwd + dgrad + wgrad) + causal attention (QK^T, PV fwd; 5 bwd
             # products with the dQ-kernel recompute counted as in the kernels)
