@@ -60,7 +60,7 @@ def parse_args(argv=None):
     p.add_argument("--sample-hz", type=float, default=1000.0)
     p.add_argument("--pack-batch", type=int, default=32)
     p.add_argument("--gather-mode", default="gather", choices=["gather", "allgather", "shm", "none"])
-    p.add_argument("--counter-set", default="lite", help="lite (default) | full | core | comma list")
+    p.add_argument("--counter-set", default="lite", help="lite (default) | full | lean | core | comma list")
     p.add_argument("--no-agent", action="store_true", help="run the workload only")
     p.add_argument("--optimizer", default="fused", choices=["fused", "torch"],
                    help="fused: one-launch CDNA4 AdamW (dynolog_amd.ops.optim); torch: AdamW(fused=True)")

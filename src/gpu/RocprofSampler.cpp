@@ -55,6 +55,13 @@ std::vector<std::string> counterNamesForSet(const std::string& set, std::string*
     disable({DC_TCC_EA0_RDREQ_32B, DC_TCC_EA0_WRREQ_64B});
     return names;
   }
+  if (set == "lean") {
+    // MFMA utilisation + bf16 rate, HBM read/write, GPU busy: the per-sample
+    // cost is mostly per SQ instance (profiles/round2/g18), so keep 2 of 8
+    disable({DC_SQ_WAVES, DC_SQ_BUSY_CYCLES, DC_SQ_WAVE_CYCLES, DC_SQ_INSTS_LDS, DC_SQ_LDS_BANK_CONFLICT,
+             DC_SQ_LDS_IDX_ACTIVE, DC_TCC_EA0_WRREQ_64B, DC_TCC_EA0_RDREQ_32B});
+    return names;
+  }
   if (set == "core") {
     disable({DC_TCC_EA0_RDREQ, DC_TCC_EA0_WRREQ, DC_TCC_EA0_WRREQ_64B, DC_TCC_EA0_RDREQ_32B});
     return names;

@@ -123,6 +123,8 @@ class CounterSampler {
 // instance measured, profiles/round1/counter_set_latency.md):
 //   full    14 counters, 784 instances on MI355X
 //   lite    drops TCC_EA0_RDREQ_32B / TCC_EA0_WRREQ_64B (528 instances)
+//   lean    MFMA busy + bf16 MOPS, TCC read/write requests, GRBM (336
+//           instances): ~half the 1 kHz overhead of lite (profiles/round2/g18)
 //   core    SQ + GRBM only, no HBM traffic (272 instances)
 //   or a comma list of canonical counter names.
 // Returns DynoCounter-ordered names with "" for disabled slots.

@@ -362,3 +362,33 @@ def test_agent_restart_returns_device_memory(native_built):
     assert all(t > 50 for t in res["taken"]), res["taken"]
     # the ring alone is ~400 MB; allow allocator noise well below one ring
     assert free[0] - min(free[1:]) < 64 << 20, free
+
+
+def test_lean_counter_set_keeps_mfma_and_hbm(native_built):
+    """--counter-set lean (2 SQ + 2 TCC + GRBM = 336 instances): cheaper
+    samples, still MFMA utilisation / bf16 rate and HBM traffic."""
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit()
+        import json, time, torch
+        torch.cuda.set_device(0)
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, counter_set="lean", sinks=("memory",))
+        x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+        end = time.time() + 1.0
+        while time.time() < end:
+            for _ in range(10):
+                y = x @ x
+            torch.cuda.synchronize()
+            a.step()
+        a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+        st = a.stats(); last = a.latest(0)
+        a.stop()
+        print("RESULT " + json.dumps(dict(stats=st, last=last)))
+    """)
+    st, last = res["stats"], res["last"]
+    assert st["raw_instances"] == 336, st["raw_instances"]
+    assert st["samples_failed"] == 0 and st["samples_taken"] > 500, st
+    assert set(st["counters"]) == {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+                                   "TCC_EA0_RDREQ", "TCC_EA0_WRREQ", "GRBM_GUI_ACTIVE", "GRBM_COUNT"}
+    assert last["mfma_util"] > 5.0 and last["mfma_bf16_tflops"] > 50.0, last
+    assert last["hbm_read_gbps"] > 0.0, last
