@@ -532,12 +532,15 @@ void Agent::samplerLoop() {
     if (now < next) {
       timespec ts{static_cast<time_t>(next / 1000000000ull), static_cast<long>(next % 1000000000ull)};
       clock_nanosleep(CLOCK_MONOTONIC, TIMER_ABSTIME, &ts, nullptr);
-    } else if (now - next > period) {
+    } else if (now - next > kMaxCatchUpTicks * period) {
       lateTicks_++;
-      next = now;  // more than a tick behind: drop the missed ticks, do not burst
+      next = now;  // far behind (a stall): drop the missed ticks rather than burst
+    } else if (now - next > period) {
+      lateTicks_++;  // a slow sample or two: catch up below
     }
-    // less than a tick behind (one slow sample): sample again right away and
-    // keep the schedule's phase, so the achieved rate stays at the target
+    // up to kMaxCatchUpTicks behind (one or two slow samples, e.g. a 1.2 ms
+    // read at 1 kHz): sample again right away and keep the schedule's phase,
+    // so the achieved rate stays at the target
   }
   if (staged > 0 && flushBatch(staged, &err)) staged = 0;
   hipWarn(hipStreamSynchronize(packStream_), "pack stream sync");

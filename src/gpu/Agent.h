@@ -130,6 +130,8 @@ class Agent {
   std::atomic<bool> gatherFailed_{false};
   std::atomic<uint64_t> flushReq_{0}, flushAck_{0};
   std::atomic<uint64_t> periodNs_{1000000};
+  // a sampler this many periods behind drops the missed ticks; less is caught up
+  static constexpr uint64_t kMaxCatchUpTicks = 4;
   std::thread samplerThread_, consumerThread_, ctlThread_;
   std::unique_ptr<ipc::Fabric> ctl_;
 
