@@ -12,6 +12,7 @@
 #include "collectors/gpu/Topology.h"
 #include "common/Logging.h"
 #include "common/Sync.h"
+#include "gpu/KernelCounters.h"
 #include "gpu/KernelTracer.h"
 #include "gpu/ShmGather.h"
 #include "ipc/Fabric.h"
@@ -881,6 +882,89 @@ void Agent::controlLoop() {
       (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, res.dump()), msg->src, 3, 10000);
     }
   }
+}
+
+Json Agent::kernelCounters(size_t top, std::string* err) const {
+  if (cfg_.rank != 0) {
+    if (err) *err = "per-kernel counters need this rank's samples, which are gathered to rank 0";
+    return Json();
+  }
+  auto& kt = KernelTracer::get();
+  const auto [w0, w1] = kt.window();
+  const int myAgent = sampler_ ? sampler_->agent().index : -1;
+  std::vector<KcSpan> spans;
+  std::map<uint64_t, uint32_t> clsOf;
+  std::vector<uint64_t> kernelOf;
+  std::vector<uint64_t> calls;
+  for (const auto& r : kt.records()) {
+    if (myAgent >= 0 && r.agentIndex >= 0 && r.agentIndex != myAgent) continue;
+    auto it = clsOf.find(r.kernelId);
+    if (it == clsOf.end()) {
+      it = clsOf.emplace(r.kernelId, static_cast<uint32_t>(kernelOf.size())).first;
+      kernelOf.push_back(r.kernelId);
+      calls.push_back(0);
+    }
+    calls[it->second]++;
+    spans.push_back({r.startNs, r.endNs, it->second});
+  }
+  std::vector<KcSample> samples;
+  {
+    std::lock_guard<std::mutex> lk(aggMu_);
+    if (agg_.world() > 0)
+      for (const auto& t : agg_.rank(0).hist) {
+        if (t.ts < w0 || t.dtUs <= 0) continue;
+        // the counters were latched somewhere inside the read that ended at
+        // ts: centre the interval on the reads (host stamps are taken after)
+        const uint64_t dt = static_cast<uint64_t>(t.dtUs * 1e3);
+        const uint64_t end = t.ts - static_cast<uint64_t>(t.latUs * 0.5e3);
+        if (end - dt > w1) break;
+        KcSample k;
+        k.t0 = end - dt;
+        k.t1 = end;
+        k.v[KC_BUSY] = t.gpuBusy;
+        k.v[KC_MFMA] = t.mfmaUtil * t.gpuBusy * 0.01;  // % of wall time (additive)
+        k.v[KC_TFLOPS] = t.tflops;
+        k.v[KC_HBM_READ] = t.hbmRead;
+        k.v[KC_HBM_WRITE] = t.hbmWrite;
+        samples.push_back(k);
+      }
+  }
+  if (samples.size() < 8 || spans.empty()) {
+    if (err) *err = "need a kernel trace window with the agent sampling (" + std::to_string(samples.size()) +
+                    " samples, " + std::to_string(spans.size()) + " dispatches)";
+    return Json();
+  }
+  const KcResult res = attributeCounters(spans, static_cast<uint32_t>(kernelOf.size()), samples);
+  std::vector<uint32_t> order(kernelOf.size());
+  for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::sort(order.begin(), order.end(),
+            [&](uint32_t a, uint32_t b) { return res.classes[a].kernelNs > res.classes[b].kernelNs; });
+  auto metrics = [](const double* v) {
+    Json m = Json::object();
+    for (int i = 0; i < KC_NUM; ++i) m[kcMetricName(i)] = v[i];
+    return m;
+  };
+  Json j = Json::object();
+  j["samples"] = static_cast<unsigned long long>(res.samples);
+  j["dispatches"] = static_cast<unsigned long long>(spans.size());
+  j["method"] = "non-negative least squares over sample intervals (rate while each kernel runs)";
+  j["r2"] = metrics(res.r2);
+  j["idle"] = metrics(res.idleRate);
+  Json ks = Json::array();
+  for (size_t i = 0; i < order.size() && i < top; ++i) {
+    const auto& c = res.classes[order[i]];
+    Json k = Json::object();
+    k["name"] = kt.kernelName(kernelOf[order[i]]);
+    k["calls"] = static_cast<unsigned long long>(calls[order[i]]);
+    k["kernel_ms"] = c.kernelNs * 1e-6;
+    k["solved"] = c.solved;
+    k["purity"] = c.purity;
+    k["counters"] = metrics(c.rate);
+    k["mixed"] = metrics(c.mixed);
+    ks.push_back(k);
+  }
+  j["kernels"] = ks;
+  return j;
 }
 
 void Agent::stop() {

@@ -99,6 +99,10 @@ class Agent {
   std::vector<Json> counterTrackEvents(uint64_t t0, uint64_t t1) const;
   // Kernel trace Chrome JSON with this agent's counter tracks under it.
   bool writeKernelTrace(const std::string& path, std::string* err) const;
+  // Per-kernel counters of the last kernel-trace window: this process's
+  // dispatches on its GPU x this rank's 1 kHz samples, de-mixed by
+  // KernelCounters (rank 0 holds its own samples; world 1 or rank 0 only).
+  Json kernelCounters(size_t top, std::string* err) const;
   void stop();
   bool running() const { return running_; }
 

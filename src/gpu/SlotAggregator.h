@@ -42,6 +42,8 @@ struct PhaseAggregate {
 struct TraceSample {
   uint64_t ts = 0;  // host_ts_ns (CLOCK_MONOTONIC)
   float gpuBusy = 0, mfmaUtil = 0, tflops = 0, hbmRead = 0, hbmWrite = 0, sclk = 0;
+  float dtUs = 0;   // interval the deltas cover (ends at ts)
+  float latUs = 0;  // time the read took (the counters were latched inside it)
   uint32_t phase = 0;
 };
 

@@ -1,6 +1,8 @@
 // Host side of the GPU agent's multi-rank path, on CPU: the rank-0 slot
 // aggregation that the RCCL gather feeds (src/gpu/SlotAggregator.h), with a
 // synthetic world-8 gather laid out exactly as ncclGather delivers it.
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -9,6 +11,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include "gpu/KernelCounters.h"
 #include "gpu/ShmGather.h"
 #include "gpu/SlotAggregator.h"
 #include "sinks/Logger.h"
@@ -220,4 +223,97 @@ TEST(GpuHost, ShmGatherMailboxAcrossProcesses) {
   // a late opener of a missing segment times out with a reason
   EXPECT_TRUE(ShmGather::open(name + "_missing", 20, &err) == nullptr);
   EXPECT_NE(err.find("not created"), std::string::npos);
+}
+
+// Per-kernel counters from 1 kHz device-wide samples (gpu/KernelCounters.h):
+// two kernel classes alternating faster than the sample period are
+// de-mixed by the non-negative least-squares fit.
+namespace {
+struct KcTruth {
+  double r[KC_NUM];
+};
+std::vector<KcSample> kcSamplesFor(const std::vector<KcSpan>& spans, const KcTruth* truth,
+                                   uint64_t t0, uint64_t t1, uint64_t period, double noise) {
+  std::vector<KcSample> out;
+  uint32_t lcg = 12345;
+  for (uint64_t a = t0; a + period <= t1; a += period) {
+    KcSample s;
+    s.t0 = a;
+    s.t1 = a + period;
+    double amt[KC_NUM] = {};
+    for (const auto& sp : spans) {
+      const uint64_t x = std::max(sp.start, s.t0), y = std::min(sp.end, s.t1);
+      if (y > x)
+        for (int m = 0; m < KC_NUM; ++m) amt[m] += static_cast<double>(y - x) * truth[sp.cls].r[m];
+    }
+    for (int m = 0; m < KC_NUM; ++m) {
+      lcg = lcg * 1664525u + 1013904223u;
+      const double u = (static_cast<double>(lcg >> 8) / static_cast<double>(1u << 24)) * 2.0 - 1.0;
+      s.v[m] = amt[m] / static_cast<double>(period) * (1.0 + noise * u);
+    }
+    out.push_back(s);
+  }
+  return out;
+}
+}  // namespace
+
+TEST(GpuHost, KernelCountersDemixInterleavedClasses) {
+  // GEMM-like class 0 (0.35 ms) and copy-like class 1 (0.2 ms) alternate with
+  // 50 us gaps; samples every 1 ms never line up with a kernel boundary.
+  const KcTruth truth[2] = {{{100, 70, 1400, 300, 50}}, {{100, 0, 0, 4000, 3500}}};
+  std::vector<KcSpan> spans;
+  const uint64_t T0 = 1000000000ull;
+  uint64_t t = T0;
+  while (t < T0 + 2000000000ull) {
+    spans.push_back({t, t + 350000, 0});
+    t += 350000 + 50000;
+    spans.push_back({t, t + 200000, 1});
+    t += 200000 + 50000;
+  }
+  for (double noise : {0.0, 0.05}) {
+    auto samples = kcSamplesFor(spans, truth, T0, t, 1000000, noise);
+    KcResult r = attributeCounters(spans, 2, samples);
+    ASSERT_EQ(r.classes.size(), 2u);
+    EXPECT_TRUE(r.classes[0].solved && r.classes[1].solved);
+    const double tol = noise > 0 ? 0.05 : 0.005;
+    for (int c = 0; c < 2; ++c)
+      for (int m = 0; m < KC_NUM; ++m) {
+        const double want = truth[c].r[m], got = r.classes[c].rate[m];
+        EXPECT_LE(std::fabs(got - want), tol * std::max(want, 100.0));
+      }
+    for (int m = 0; m < KC_NUM; ++m) EXPECT_LE(r.idleRate[m], noise > 0 ? 60.0 : 1.0);
+    if (noise == 0.0) {
+      EXPECT_GT(r.r2[KC_HBM_READ], 0.999);
+      // the plain overlap-weighted mean blends the classes; the fit does not
+      EXPECT_GT(r.classes[0].mixed[KC_HBM_READ], 1000.0);
+      EXPECT_GT(r.classes[1].mixed[KC_MFMA], 10.0);
+      EXPECT_LT(r.classes[0].purity, 0.8);
+    }
+  }
+}
+
+TEST(GpuHost, KernelCountersPoolRareClasses) {
+  // class 2 runs 0.1 ms in total: below minCover it is not solved for, its
+  // rates fall back to the mixed mean and the fit of the others still holds
+  const KcTruth truth[3] = {{{100, 60, 1200, 200, 100}}, {{100, 0, 0, 3000, 3000}}, {{100, 5, 10, 50, 50}}};
+  std::vector<KcSpan> spans;
+  const uint64_t T0 = 5000000000ull;
+  uint64_t t = T0;
+  for (int i = 0; i < 3000; ++i) {
+    spans.push_back({t, t + 300000, 0});
+    t += 300000;
+    spans.push_back({t, t + 250000, 1});
+    t += 250000;
+    if (i == 1500) {
+      spans.push_back({t, t + 100000, 2});
+      t += 100000;
+    }
+  }
+  auto samples = kcSamplesFor(spans, truth, T0, t, 1000000, 0.0);
+  KcResult r = attributeCounters(spans, 3, samples);
+  EXPECT_TRUE(r.classes[0].solved && r.classes[1].solved);
+  EXPECT_FALSE(r.classes[2].solved);
+  EXPECT_LE(std::fabs(r.classes[0].rate[KC_TFLOPS] - 1200.0), 20.0);
+  EXPECT_LE(std::fabs(r.classes[1].rate[KC_HBM_WRITE] - 3000.0), 50.0);
+  EXPECT_GT(r.classes[2].kernelNs, 0.0);
 }

@@ -392,3 +392,48 @@ def test_lean_counter_set_keeps_mfma_and_hbm(native_built):
                                    "TCC_EA0_RDREQ", "TCC_EA0_WRREQ", "GRBM_GUI_ACTIVE", "GRBM_COUNT"}
     assert last["mfma_util"] > 5.0 and last["mfma_bf16_tflops"] > 50.0, last
     assert last["hbm_read_gbps"] > 0.0, last
+
+
+def test_kernel_counters_demix_gemm_and_copy(native_built):
+    """Per-kernel counters from the 1 kHz samples (KernelTrace.counters): a
+    bf16 GEMM and an HBM copy alternate faster than the sample period; the
+    least-squares fit gives the GEMM the MFMA activity and the copy the HBM
+    traffic, which the plain overlap-weighted means blend."""
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit(kernel_trace=True)
+        import json, time, torch
+        torch.cuda.set_device(0)
+        ag = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
+        a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+        src = torch.randn(256 << 20, device="cuda", dtype=torch.bfloat16)
+        dst = torch.empty_like(src)
+        y = a @ a; dst.copy_(src); torch.cuda.synchronize()
+        with agent.KernelTrace() as kt:
+            t0 = time.time()
+            while time.time() - t0 < 1.5:
+                for _ in range(8):
+                    y = a @ a
+                    dst.copy_(src)
+                    dst.copy_(src)
+                ag.step()
+                torch.cuda.synchronize()
+        ag.pack_pending(); ag.step(); torch.cuda.synchronize(); ag.flush()
+        time.sleep(0.2)
+        c = kt.counters(top=10)
+        ag.stop()
+        print("RESULT " + json.dumps(c))
+    """)
+    ks = res["kernels"]
+    gemm = [k for k in ks if "Cijk" in k["name"] or "gemm" in k["name"].lower()]
+    copy = [k for k in ks if "copy" in k["name"].lower() or "elementwise" in k["name"].lower()]
+    assert gemm and copy, [k["name"] for k in ks]
+    g, c = gemm[0], copy[0]
+    assert res["samples"] > 800 and g["solved"] and c["solved"], res
+    gc, cc = g["counters"], c["counters"]
+    assert gc["mfma_busy_pct"] > 20.0 and gc["bf16_tflops"] > 300.0, g
+    assert cc["mfma_busy_pct"] < 0.2 * gc["mfma_busy_pct"], (g, c)
+    assert cc["hbm_read_gbps"] > 1500.0 and cc["hbm_read_gbps"] > 2.0 * gc["hbm_read_gbps"], (g, c)
+    # the fit separates what the overlap-weighted mean mixes
+    assert cc["mfma_busy_pct"] < c["mixed"]["mfma_busy_pct"], c
+    assert res["r2"]["hbm_read_gbps"] > 0.5 and res["r2"]["mfma_busy_pct"] > 0.5, res["r2"]
