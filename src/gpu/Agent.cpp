@@ -763,23 +763,27 @@ std::vector<Json> Agent::counterTrackEvents(uint64_t t0, uint64_t t1) const {
   return agg_.counterTrackEvents(t0, t1, static_cast<int>(getpid()));
 }
 
+void Agent::waitSamplesThrough(uint64_t t1) const {
+  // the window's last samples reach rank 0 with the next step()'s gather:
+  // give the training loop up to 1 s to deliver them
+  const uint64_t deadline = monoNs() + 1000000000ull;
+  while (cfg_.rank == 0 && running_ && !paused_ && monoNs() < deadline) {
+    {
+      std::lock_guard<std::mutex> lk(aggMu_);
+      uint64_t oldest = UINT64_MAX;
+      for (int r = 0; r < agg_.world(); ++r) oldest = std::min(oldest, agg_.rank(r).last.host_ts_ns);
+      if (oldest >= t1) break;
+    }
+    usleep(20000);
+  }
+}
+
 bool Agent::writeKernelTrace(const std::string& path, std::string* err) const {
   auto& kt = KernelTracer::get();
   std::vector<Json> tracks;
   if (running_) {
     const auto [t0, t1] = kt.window();
-    // the window's last samples reach rank 0 with the next step()'s gather:
-    // give the training loop up to 1 s to deliver them
-    const uint64_t deadline = monoNs() + 1000000000ull;
-    while (cfg_.rank == 0 && !paused_ && monoNs() < deadline) {
-      {
-        std::lock_guard<std::mutex> lk(aggMu_);
-        uint64_t oldest = UINT64_MAX;
-        for (int r = 0; r < agg_.world(); ++r) oldest = std::min(oldest, agg_.rank(r).last.host_ts_ns);
-        if (oldest >= t1) break;
-      }
-      usleep(20000);
-    }
+    waitSamplesThrough(t1);
     tracks = counterTrackEvents(t0, t1);
     if (!tracks.empty()) {
       Json m = Json::object();
@@ -871,6 +875,15 @@ void Agent::controlLoop() {
         kt.stop(&err);
         res["status"] = "ok";
         res["summary"] = kt.summary(static_cast<size_t>(std::max(top, 1)));
+        if (cfg_.rank == 0 && !paused_) {
+          // per-kernel counters from this window's 1 kHz samples (KernelCounters)
+          packPending();
+          waitSamplesThrough(kt.window().second);
+          std::string cerr;
+          Json kc = kernelCounters(static_cast<size_t>(std::max(top, 1)), &cerr);
+          if (!kc.isNull()) res["kernel_counters"] = kc;
+          else res["kernel_counters_error"] = cerr;
+        }
         if (req.contains("chrome_path") && req.at("chrome_path").isString()) {
           const std::string path = req.at("chrome_path").asString();
           // flush pending samples so the counter tracks cover the window
@@ -934,7 +947,39 @@ Json Agent::kernelCounters(size_t top, std::string* err) const {
                     " samples, " + std::to_string(spans.size()) + " dispatches)";
     return Json();
   }
-  const KcResult res = attributeCounters(spans, static_cast<uint32_t>(kernelOf.size()), samples);
+  // The dispatch stamps (GPU ticks converted by the runtime) and the sample
+  // stamps (host clock after each read returns; the counters were latched at
+  // an unknown point inside the ~100-300 us read) do not line up to the
+  // tens of microseconds this needs.  Calibrate: shift the dispatches by
+  // -2..+2 ms in 25 us steps and keep the shift whose fit explains the
+  // samples best (mean R^2 over the metrics); report it.
+  const uint32_t nCls = static_cast<uint32_t>(kernelOf.size());
+  auto fitAt = [&](int64_t shiftNs) {
+    std::vector<KcSpan> sh(spans);
+    for (auto& sp : sh) {
+      sp.start = static_cast<uint64_t>(static_cast<int64_t>(sp.start) + shiftNs);
+      sp.end = static_cast<uint64_t>(static_cast<int64_t>(sp.end) + shiftNs);
+    }
+    return attributeCounters(sh, nCls, samples);
+  };
+  auto score = [](const KcResult& r) {  // busy share barely varies: not scored
+    double s = 0;
+    for (int m = KC_MFMA; m < KC_NUM; ++m) s += r.r2[m];
+    return s / (KC_NUM - KC_MFMA);
+  };
+  int64_t bestShift = 0;
+  KcResult res = fitAt(0);
+  double best = score(res);
+  for (int64_t sh = -2000000; sh <= 2000000; sh += 25000) {
+    if (sh == 0) continue;
+    KcResult r = fitAt(sh);
+    const double sc = score(r);
+    if (sc > best) {
+      best = sc;
+      bestShift = sh;
+      res = std::move(r);
+    }
+  }
   std::vector<uint32_t> order(kernelOf.size());
   for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
   std::sort(order.begin(), order.end(),
@@ -948,6 +993,8 @@ Json Agent::kernelCounters(size_t top, std::string* err) const {
   j["samples"] = static_cast<unsigned long long>(res.samples);
   j["dispatches"] = static_cast<unsigned long long>(spans.size());
   j["method"] = "non-negative least squares over sample intervals (rate while each kernel runs)";
+  j["clock_shift_us"] = static_cast<double>(bestShift) * 1e-3;
+  j["fit_score"] = best;
   j["r2"] = metrics(res.r2);
   j["idle"] = metrics(res.idleRate);
   Json ks = Json::array();

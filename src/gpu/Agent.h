@@ -121,6 +121,7 @@ class Agent {
   void logInterval();
   bool setupLayout(const std::vector<uint64_t>& ids, std::string* err);
   void releaseDevice();
+  void waitSamplesThrough(uint64_t t1) const;  // rank 0: samples up to t1 ingested (<= 1 s)
   std::unique_ptr<Logger> makeLogger();
 
   AgentConfig cfg_;

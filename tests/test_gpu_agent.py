@@ -405,17 +405,17 @@ def test_kernel_counters_demix_gemm_and_copy(native_built):
         import json, time, torch
         torch.cuda.set_device(0)
         ag = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
-        a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
-        src = torch.randn(256 << 20, device="cuda", dtype=torch.bfloat16)
+        a = torch.randn(16384, 16384, device="cuda", dtype=torch.bfloat16)
+        src = torch.randn(1 << 30, device="cuda", dtype=torch.bfloat16)
         dst = torch.empty_like(src)
         y = a @ a; dst.copy_(src); torch.cuda.synchronize()
         with agent.KernelTrace() as kt:
             t0 = time.time()
-            while time.time() - t0 < 1.5:
-                for _ in range(8):
-                    y = a @ a
-                    dst.copy_(src)
-                    dst.copy_(src)
+            while time.time() - t0 < 2.0:
+                for _ in range(4):
+                    y = a @ a            # ~6 ms of MFMA work
+                    for _ in range(4):
+                        dst.copy_(src)   # 4 x 4 GB of HBM traffic
                 ag.step()
                 torch.cuda.synchronize()
         ag.pack_pending(); ag.step(); torch.cuda.synchronize(); ag.flush()
@@ -433,7 +433,10 @@ def test_kernel_counters_demix_gemm_and_copy(native_built):
     gc, cc = g["counters"], c["counters"]
     assert gc["mfma_busy_pct"] > 20.0 and gc["bf16_tflops"] > 300.0, g
     assert cc["mfma_busy_pct"] < 0.2 * gc["mfma_busy_pct"], (g, c)
-    assert cc["hbm_read_gbps"] > 1500.0 and cc["hbm_read_gbps"] > 2.0 * gc["hbm_read_gbps"], (g, c)
+    assert cc["bf16_tflops"] < 0.25 * gc["bf16_tflops"], (g, c)
+    # "HBM" reads are TCC EA (L2-miss) requests, which a GEMM streaming its
+    # panels through L2 also makes in volume (MALL hits); writes separate
+    assert cc["hbm_write_gbps"] > 1000.0 and cc["hbm_write_gbps"] > 2.0 * gc["hbm_write_gbps"], (g, c)
     # the fit separates what the overlap-weighted mean mixes
-    assert cc["mfma_busy_pct"] < c["mixed"]["mfma_busy_pct"], c
-    assert res["r2"]["hbm_read_gbps"] > 0.5 and res["r2"]["mfma_busy_pct"] > 0.5, res["r2"]
+    assert cc["bf16_tflops"] < c["mixed"]["bf16_tflops"], c
+    assert res["r2"]["bf16_tflops"] > 0.6 and res["r2"]["hbm_write_gbps"] > 0.6, res["r2"]
