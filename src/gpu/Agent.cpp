@@ -1006,6 +1006,9 @@ Json Agent::kernelCounters(size_t top, std::string* err) const {
     k["kernel_ms"] = c.kernelNs * 1e-6;
     k["solved"] = c.solved;
     k["purity"] = c.purity;
+    // kernels far shorter than a sample interval are not separable from
+    // their neighbours (purity = kernel time / time of the touched intervals)
+    k["resolved"] = c.solved && c.purity >= 0.1;
     k["counters"] = metrics(c.rate);
     k["mixed"] = metrics(c.mixed);
     ks.push_back(k);

@@ -429,7 +429,7 @@ def test_kernel_counters_demix_gemm_and_copy(native_built):
     copy = [k for k in ks if "copy" in k["name"].lower() or "elementwise" in k["name"].lower()]
     assert gemm and copy, [k["name"] for k in ks]
     g, c = gemm[0], copy[0]
-    assert res["samples"] > 800 and g["solved"] and c["solved"], res
+    assert res["samples"] > 800 and g["resolved"] and c["resolved"], res
     gc, cc = g["counters"], c["counters"]
     assert gc["mfma_busy_pct"] > 20.0 and gc["bf16_tflops"] > 300.0, g
     assert cc["mfma_busy_pct"] < 0.2 * gc["mfma_busy_pct"], (g, c)

@@ -71,7 +71,8 @@ def main() -> int:
         c = k["counters"]
         print(f"{k['name'][:60]:60s} {k['calls']:6d} {k['kernel_ms']:8.1f} {k['purity']:6.2f} "
               f"{c['mfma_busy_pct']:6.1f} {c['bf16_tflops']:7.0f} {c['hbm_read_gbps']:7.0f} "
-              f"{c['hbm_write_gbps']:7.0f}{'' if k['solved'] else '  (mixed)'}")
+              f"{c['hbm_write_gbps']:7.0f}"
+              f"{'' if k['resolved'] else ('  (unresolved)' if k['solved'] else '  (mixed)')}")
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
