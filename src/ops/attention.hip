@@ -522,13 +522,11 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv8_kernel(
 
     for (int it = 0; it < niter; ++it) {
       unsigned char* st = stages + (it & 1) * BSTAGE;
-      if (it + 1 < niter) {
-        issue(it + 1, stages + ((it + 1) & 1) * BSTAGE);
-        if (w < 2) WAIT_VM(5); else WAIT_VM(4);
-      } else {
-        WAIT_VM(0);
-      }
+      // this stage's DMA (issued under the previous compute) has landed for
+      // every wave, and every wave is done with the other stage: one barrier
+      WAIT_VM(0);
       __syncthreads();
+      if (it + 1 < niter) issue(it + 1, stages + ((it + 1) & 1) * BSTAGE);
       const unsigned char* qi = st;
       const unsigned char* di = st + FTILE;
       const float* lsel = reinterpret_cast<const float*>(st + 2 * FTILE);
@@ -589,10 +587,11 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv8_kernel(
             dka[dt] = mfma(tr_read(qi, 32 * qh + 16 * ks, 32 * dt, lane), zb[ks], dka[dt]);
           }
       }
-      __syncthreads();
     }
+    // every wave done with the K/V images and stages before they are reused
+    __syncthreads();
     // combine the two query halves of each key group through LDS (all DMA
-    // drained by the last WAIT_VM(0); the loop's final barrier fenced reads)
+    // drained by the last WAIT_VM(0))
     float* red = reinterpret_cast<float*>(smem) + kg * (128 * 64);
     if (qh == 1) {
 #pragma unroll
@@ -676,15 +675,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(
     const int k0 = t * FK;
     unsigned char* kt = smem + (t & 1) * 2 * FTILE;
     unsigned char* vt = kt + FTILE;
+    WAIT_VM(0);
+    __syncthreads();  // tile t landed for all waves; all done with tile t-1's buffer
     if (t + 1 < ntiles) {
       unsigned char* nk = smem + ((t + 1) & 1) * 2 * FTILE;
       dma_tile<FK>(kb + (size_t)(k0 + FK) * kvs, kvs, nk, w, lane);
       dma_tile<FK>(vb + (size_t)(k0 + FK) * kvs, kvs, nk + FTILE, w, lane);
-      WAIT_VM(8);
-    } else {
-      WAIT_VM(0);
     }
-    __syncthreads();
     if (k0 <= qw0 + 31) {
       // One 32-key half at a time keeps the live set at two accumulators plus
       // 8 operand fragments (fits 256 VGPRs: two waves per SIMD).
@@ -728,7 +725,6 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) dqa[dt] = mfma(tr_read(kt, 16 * ks, 32 * dt, lane), zb[ks], dqa[dt]);
     }
-    __syncthreads();
   }
   u16* op = dq + ((size_t)(b * S + qrow) * H + head) * HD;
 #pragma unroll
