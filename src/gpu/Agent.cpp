@@ -203,6 +203,37 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   }
   releaseDevice();
 
+  // RCCL path: every multi-rank run, and world 1 with force_collective (a
+  // 1-rank communicator, so the collective code runs on a one-GPU box too).
+  // The communicator comes up FIRST, before any local step that can fail:
+  // ncclCommInitRank blocks until every rank has called it, so a rank that
+  // failed earlier (an unsupported counter, an allocation) would leave the
+  // others waiting forever.  From here on every rank returns, and agent.py
+  // all-gathers the outcomes and falls back together.
+  shmMode_ = cfg_.gatherMode == "shm" && cfg_.world > 1;
+  collective_ = (cfg_.world > 1 || cfg_.forceCollective) && cfg_.gatherMode != "none" && !shmMode_;
+  if (collective_) {
+    ncclUniqueId id;
+    if (cfg_.world == 1 && (!uid || idLen == 0)) {
+      ncclResult_t g = ncclGetUniqueId(&id);
+      if (g != ncclSuccess) {
+        *err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(g);
+        return false;
+      }
+    } else if (!uid || idLen != sizeof(ncclUniqueId)) {
+      *err = "world > 1 requires an ncclUniqueId of " + std::to_string(sizeof(ncclUniqueId)) +
+             " bytes";
+      return false;
+    } else {
+      memcpy(&id, uid, sizeof(id));
+    }
+    ncclResult_t r = ncclCommInitRank(&comm_, cfg_.world, id, cfg_.rank);
+    if (r != ncclSuccess) {
+      *err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+      return false;
+    }
+  }
+
   // map HIP device -> rocprofiler agent by PCI location
   int agentIdx = cfg_.agentIndex;
   if (agentIdx < 0) {
@@ -276,7 +307,6 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   sendBytes_ = sizeof(DynoGatherHeader) + static_cast<size_t>(cfg_.gatherCapSlots) * sizeof(DynoSlot);
   HIP_OK(hipMalloc(&dSend_, sendBytes_), "hipMalloc send");
   const bool root = cfg_.rank == 0;
-  shmMode_ = cfg_.gatherMode == "shm" && cfg_.world > 1;
   // shm mode: rank 0 drains only its own block; the peers' come through the mailbox
   const size_t recvBytes = shmMode_ ? (root ? sendBytes_ : 0)
                            : (cfg_.gatherMode == "allgather" || root) ? sendBytes_ * static_cast<size_t>(cfg_.world)
@@ -294,9 +324,6 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     }
   }
 
-  // RCCL path: every multi-rank run, and world 1 with force_collective (a
-  // 1-rank communicator, so the collective code runs on a one-GPU box too)
-  collective_ = (cfg_.world > 1 || cfg_.forceCollective) && cfg_.gatherMode != "none" && !shmMode_;
   if (shmMode_) {
     // segment name from the id rank 0 broadcast (agent.py), identical on every rank
     if (!uid || idLen < 8) {
@@ -315,27 +342,6 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
       HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&shmDev_), shm_->base(), 0), "mailbox device ptr");
     }
     shmEnq_ = 0;
-  }
-  if (collective_) {
-    ncclUniqueId id;
-    if (cfg_.world == 1 && (!uid || idLen == 0)) {
-      ncclResult_t g = ncclGetUniqueId(&id);
-      if (g != ncclSuccess) {
-        *err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(g);
-        return false;
-      }
-    } else if (!uid || idLen != sizeof(ncclUniqueId)) {
-      *err = "world > 1 requires an ncclUniqueId of " + std::to_string(sizeof(ncclUniqueId)) +
-             " bytes";
-      return false;
-    } else {
-      memcpy(&id, uid, sizeof(id));
-    }
-    ncclResult_t r = ncclCommInitRank(&comm_, cfg_.world, id, cfg_.rank);
-    if (r != ncclSuccess) {
-      *err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
-      return false;
-    }
   }
 
   agg_.reset(cfg_.world, cfg_.gatherCapSlots);
