@@ -81,6 +81,9 @@ class CompositeLogger : public Logger {
 class OdsLogger : public JsonLogger {
  public:
   OdsLogger();
+  // ODS time series are numeric: string keys (job_id, username, ...) are
+  // dropped, as in the reference (ODSJsonLogger.h:16-17).
+  void logStr(const std::string&, const std::string&) override {}
   void finalize() override;
   // Builds the datapoints array without sending (exposed for tests).
   Json buildDatapoints() const;
