@@ -4,6 +4,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from dynolog_amd.utils import client
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -25,10 +27,11 @@ def test_hostlist_expansion():
 def test_unitrace_dry_run_commands(native_built, tmp_path):
     r = subprocess.run([sys.executable, os.path.join(REPO, "scripts/pytorch/unitrace.py"),
                         "--hosts", "n[1-2]", "--job-id", "42", "-o", str(tmp_path), "--iterations", "5",
-                        "--dry-run"], capture_output=True, text=True, timeout=30)
+                        "--dry-run", "--record-shapes"], capture_output=True, text=True, timeout=30)
     assert r.returncode == 0, r.stderr
     lines = r.stdout.strip().splitlines()
     assert len(lines) == 2
+    assert all(ln.endswith("--record-shapes") and "--with-stacks" not in ln for ln in lines)
     assert "--hostname n1" in lines[0] and "--job-id 42" in lines[0]
     assert "--iterations 5" in lines[0] and "--profile-start-iteration-roundup 1000" in lines[0]
     assert f"{tmp_path}/libkineto_trace_n2.json" in lines[1]
@@ -40,6 +43,10 @@ def test_client_config_matches_cli():
     cfg = client.kineto_config("/tmp/t.json", iterations=3, start_iteration_roundup=10)
     assert cfg.endswith("PROFILE_START_ITERATION_ROUNDUP=10\nACTIVITIES_ITERATIONS=3")
     assert client.trace_files("/x/t.json", [5, 6]) == ["/x/t_5.json", "/x/t_6.json"]
+    cfg = client.kineto_config("/tmp/t.json", record_shapes=True, with_stacks=False)
+    assert cfg.endswith("ACTIVITIES_DURATION_MSECS=500\nPROFILE_REPORT_INPUT_SHAPES=true")
+    with pytest.raises(TypeError):
+        client.kineto_config("/tmp/t.json", with_shapes=True)
 
 
 def test_linear_model_example_runs_on_cpu():
