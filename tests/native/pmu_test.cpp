@@ -166,12 +166,19 @@ TEST(Pmu, PerfMonitorSoftwareMetricsPerProcess) {
 }
 
 namespace {
-// Spin on the CPU for `ms` once `go` is set (a worker thread's busy loop).
+double threadCpuMs() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+// Burn `ms` of this thread's own CPU time once `go` is set (a worker thread's
+// busy loop; CPU time, not wall time, so a loaded host does not change it).
 void spinWhenReleased(const std::atomic<bool>& go, int ms) {
   while (!go.load()) usleep(500);
-  const auto end = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+  const double end = threadCpuMs() + ms;
   volatile double x = 0;
-  while (std::chrono::steady_clock::now() < end) x = x + 1.0;
+  while (threadCpuMs() < end) x = x + 1.0;
 }
 }  // namespace
 
@@ -195,16 +202,21 @@ TEST(Pmu, PerProcessTargetCountsEveryThread) {
   std::thread late([&] { spinWhenReleased(go, 150); });
   usleep(2000);
   pm.step();  // opens the late thread's groups
+  const auto t0 = std::chrono::steady_clock::now();
   EXPECT_GE(pm.threads(), 3);
   go = true;
   early.join();
   late.join();
   usleep(10000);
   pm.step();
+  const double wallS = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   const double msPerS = pm.lastOutputs().count("cpu_clock_ms_per_s") ? pm.lastOutputs().at("cpu_clock_ms_per_s") : 0.0;
-  // ~2 x 150 ms of CPU in ~0.17 s of wall: well above one core (main thread alone: ~0)
-  EXPECT_GT(msPerS, 1000.0);
-  EXPECT_LT(msPerS, 2600.0);
+  // The interval's counted CPU time is both workers' 2 x 150 ms (the main
+  // thread sleeps in join): counting only one of them, or only the main
+  // thread, would give <= ~160 ms.  CPU time, so host load does not matter.
+  const double countedMs = msPerS * wallS;
+  EXPECT_GT(countedMs, 260.0);
+  EXPECT_LT(countedMs, 360.0);
   pm.step();  // groups of the exited threads are gone: only the live threads remain
   // (the main thread, plus any runtime helper thread, e.g. TSAN's background thread)
   int live = 0;
