@@ -129,7 +129,11 @@ def main(argv=None) -> int:
     model = pdist.wrap_ddp(model, env)
     if args.optimizer == "fused":
         from dynolog_amd.ops.optim import FusedAdamW
-        opt = FusedAdamW(model.parameters(), lr=1e-5, betas=(0.9, 0.95), weight_decay=0.1)
+        from dynolog_amd.ops import dgrad_weights
+        # the update also writes W^T of every linear weight for the input-gradient
+        # GEMMs (ops.dgrad), instead of a just-in-time transpose per GEMM
+        opt = FusedAdamW(model.parameters(), lr=1e-5, betas=(0.9, 0.95), weight_decay=0.1,
+                         transposed=dgrad_weights(model))
     else:
         opt = torch.optim.AdamW(model.parameters(), lr=1e-5, betas=(0.9, 0.95),
                                 weight_decay=0.1, fused=True)

@@ -37,3 +37,29 @@ def test_model_cpu_path_is_plain_pytorch():
     assert torch.isfinite(loss)
     assert all(p.grad is not None for p in m.parameters())
     assert not llama.fused_ops_enabled(ids)
+
+
+def test_weight_transpose_registry_invalidation():
+    """ops.cached_transpose: a W^T registered by the optimizer is served until
+    the weight changes through torch (version bump), is unregistered, or is
+    freed; a shape mismatch never matches (pure host logic, CPU tensors)."""
+    w = torch.nn.Parameter(torch.randn(4, 6))
+    wt = w.detach().t().contiguous()
+    ops.register_transposed(w, wt)
+    assert ops.cached_transpose(w) is wt
+    assert ops.cached_transpose(w.detach()) is wt  # same storage, same version counter
+    with torch.no_grad():
+        w.add_(1.0)
+    assert ops.cached_transpose(w) is None  # stale after an in-place torch write
+    ops.register_transposed(w, wt)
+    ops.unregister_transposed(w)
+    assert ops.cached_transpose(w) is None
+    ops.register_transposed(w, torch.empty(4, 6))  # wrong shape for w^T
+    assert ops.cached_transpose(w) is None
+    v = torch.nn.Parameter(torch.randn(3, 3))
+    ops.register_transposed(v, v.detach().t().contiguous())
+    ptr = v.data_ptr()
+    del v
+    assert ops._WT[ptr][0]() is None  # freed weight: its entry can no longer match
+    ops.unregister_transposed(torch.empty(0))  # unknown pointer: no-op
+    assert ops.dgrad_weights(llama.build_llama("tiny", device="cpu", dtype=torch.float32)) != []
