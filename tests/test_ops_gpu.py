@@ -253,7 +253,8 @@ def test_fused_adamw_transposed_copies(ops):
             if a.dim() == 2 and a.shape[0] % 128 == 0:
                 assert wt is not None and torch.equal(wt, a.t()), f"W^T[{i}] step {step}"
             else:
-                assert wt is None and "weight_t" not in oa.state[a], i
+                assert wt is None and id(a) not in oa._wt, i
+            assert set(oa.state[a]) == {"step", "exp_avg", "exp_avg_sq"}  # state_dict stays AdamW-shaped
     # dgrad through the copy == dgrad through a fresh transpose
     w = pa[0]
     dy = torch.randn(512, w.shape[0], device=DEV, generator=g).bfloat16()
