@@ -81,6 +81,18 @@ std::unique_ptr<ShmGather> ShmGather::open(const std::string& name, int openTime
         void* b = mmap(nullptr, static_cast<size_t>(st.st_size), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         if (b != MAP_FAILED) {
           auto* h = static_cast<Header*>(b);
+          const size_t have = static_cast<size_t>(st.st_size);
+          if (reinterpret_cast<std::atomic<uint64_t>*>(&h->magic)->load(std::memory_order_acquire) == kMagic &&
+              !(h->world >= 1 && h->entries >= 1 &&
+                h->laneBytes >= sizeof(Lane) + static_cast<size_t>(h->entries) * h->blockBytes &&
+                have >= roundUp(sizeof(Header), 128) + static_cast<size_t>(h->world) * h->laneBytes)) {
+            // inconsistent geometry (a foreign or truncated segment): never hand
+            // out block pointers into it
+            munmap(b, have);
+            close(fd);
+            if (err) *err = "shm gather: open " + name + ": inconsistent segment geometry";
+            return nullptr;
+          }
           if (reinterpret_cast<std::atomic<uint64_t>*>(&h->magic)->load(std::memory_order_acquire) == kMagic) {
             close(fd);
             std::unique_ptr<ShmGather> g(new ShmGather());

@@ -1,6 +1,8 @@
 // Host side of the GPU agent's multi-rank path, on CPU: the rank-0 slot
 // aggregation that the RCCL gather feeds (src/gpu/SlotAggregator.h), with a
 // synthetic world-8 gather laid out exactly as ncclGather delivers it.
+#include <sys/mman.h>
+#include <fcntl.h>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -223,6 +225,18 @@ TEST(GpuHost, ShmGatherMailboxAcrossProcesses) {
   // a late opener of a missing segment times out with a reason
   EXPECT_TRUE(ShmGather::open(name + "_missing", 20, &err) == nullptr);
   EXPECT_NE(err.find("not created"), std::string::npos);
+  // a segment whose size no longer covers the lanes its header describes
+  // (truncated / foreign) is refused instead of handing out block pointers
+  const std::string tname = name + "_trunc";
+  auto t = ShmGather::create(tname, 8, 4, 4096, &err);
+  ASSERT_TRUE(t != nullptr);
+  int fd = shm_open(tname.c_str(), O_RDWR, 0600);
+  ASSERT_TRUE(fd >= 0);
+  ASSERT_EQ(ftruncate(fd, 8192), 0);
+  close(fd);
+  err.clear();
+  EXPECT_TRUE(ShmGather::open(tname, 20, &err) == nullptr);
+  EXPECT_NE(err.find("inconsistent"), std::string::npos);
 }
 
 // Per-kernel counters from 1 kHz device-wide samples (gpu/KernelCounters.h):
