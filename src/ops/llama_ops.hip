@@ -98,13 +98,15 @@ __global__ __launch_bounds__(kBlock) void rmsnorm_fwd_kernel(
 #pragma unroll
         for (int i = 0; i < 8; ++i) ss += v[k][i] * v[k][i];
       }
+      // w is issued before the row reduction so its (L2) latency overlaps it
+      u16x8 wp[VPL];
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) wp[k] = *reinterpret_cast<const u16x8*>(w + (k * 64 + lane) * 8);
       const float r = rsqrtf(wave_sum(ss) / float(D) + eps);
 #pragma unroll
       for (int k = 0; k < VPL; ++k) {
-        float wv[8];
-        load8(w + (k * 64 + lane) * 8, wv);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[k][i] = v[k][i] * r * wv[i];
+        for (int i = 0; i < 8; ++i) v[k][i] = v[k][i] * r * bf2f(wp[k][i]);
         store8(yr + (k * 64 + lane) * 8, v[k]);
       }
       if (lane == 0) rstd[row] = r;
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(kBlock) void rmsnorm_bwd_kernel(
   }
   int parity = 0;
   for (int row0 = blockIdx.x * kBwdRows; row0 < N; row0 += gridDim.x * kBwdRows) {
-    u16x8 xp[kBwdRows][CPT], dp[kBwdRows][CPT];
+    u16x8 xp[kBwdRows][CPT], dp[kBwdRows][CPT], rp[kBwdRows][CPT];
     float r[kBwdRows], dot[kBwdRows];
 #pragma unroll
     for (int q = 0; q < kBwdRows; ++q) {
@@ -179,6 +181,9 @@ __global__ __launch_bounds__(kBlock) void rmsnorm_bwd_kernel(
         const size_t off = size_t(row) * D + (k * kBlock + threadIdx.x) * 8;
         xp[q][k] = *reinterpret_cast<const u16x8*>(x + off);
         dp[q][k] = *reinterpret_cast<const u16x8*>(dy + off);
+        // the residual gradient is loaded with the others, not after the
+        // row reduction, so its latency hides under the reduction too
+        if (dres) rp[q][k] = *reinterpret_cast<const u16x8*>(dres + off);
       }
     }
 #pragma unroll
@@ -217,10 +222,8 @@ __global__ __launch_bounds__(kBlock) void rmsnorm_bwd_kernel(
           o[i] = r[q] * bf2f(dp[q][k][i]) * wv[k][i] - bf2f(xp[q][k][i]) * coef;
         const size_t off = size_t(row0 + q) * D + (k * kBlock + threadIdx.x) * 8;
         if (dres) {  // residual branch's gradient joins here (no separate add kernel)
-          float rv[8];
-          load8(dres + off, rv);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += rv[i];
+          for (int i = 0; i < 8; ++i) o[i] += bf2f(rp[q][k][i]);
         }
         store8(dx + off, o);
       }
