@@ -237,11 +237,15 @@ def main(argv=None) -> int:
 
         meas_s, m0, m1 = timed(args.steps)
         # per-rank time to finish its own steps inside the headline window
-        # (stragglers / imbalance show here; the window itself ends at the barrier)
-        rank_local = [local_s[0]]
+        # (stragglers / imbalance show here; the window itself ends at the barrier),
+        # and every rank's window on its own CLOCK_MONOTONIC: samples carry their
+        # own host's stamps, so rank 0 counts each rank's inside that rank's window
+        rank_local, windows = [local_s[0]], [(m0, m1)]
         if torch.distributed.is_initialized():
-            rank_local = [None] * env.world
-            torch.distributed.all_gather_object(rank_local, local_s[0])
+            gathered = [None] * env.world
+            torch.distributed.all_gather_object(gathered, (local_s[0], m0, m1))
+            rank_local = [g[0] for g in gathered]
+            windows = [(g[1], g[2]) for g in gathered]
         loss_val = float(last_loss[0].item()) if torch.is_tensor(last_loss[0]) else last_loss[0]
 
         total_samples = 0
@@ -256,7 +260,7 @@ def main(argv=None) -> int:
             pdist.barrier()
             if env.rank == 0:
                 ag.flush()
-                per_rank = ag.window_counts(m0, m1)
+                per_rank = ag.window_counts([w[0] for w in windows], [w[1] for w in windows])
                 total_samples = sum(per_rank)
                 agent_stats = ag.stats()
             if base_s is not None:
@@ -372,6 +376,10 @@ def main(argv=None) -> int:
                     train_step()
                 torch.cuda.synchronize()
                 s, a0, a1 = timed(args.steps)
+                wins = [(a0, a1)]
+                if torch.distributed.is_initialized():
+                    wins = [None] * env.world
+                    torch.distributed.all_gather_object(wins, (a0, a1))
                 ag.pack_pending()
                 pdist.barrier()
                 ag.step()
@@ -380,7 +388,7 @@ def main(argv=None) -> int:
                 n = 0
                 if env.rank == 0:
                     ag.flush()
-                    n = sum(ag.window_counts(a0, a1))
+                    n = sum(ag.window_counts([w[0] for w in wins], [w[1] for w in wins]))
                 row = {"sample_hz_target": hz, "ms_per_step": round(s / args.steps * 1e3, 3),
                        "overhead_pct": round((s / base_s - 1.0) * 100.0, 3) if base_s else None,
                        "samples_per_sec_per_gpu": round(n / ((a1 - a0) * 1e-9) / env.world, 2)}
