@@ -174,7 +174,7 @@ Json DeviceMonitor::drainRecords() {
       for (int d = 0; d < DD_NUM_DERIVED; ++d) r[names[static_cast<size_t>(d)]] = g->derivedSum[d] / n;
       for (int c = 0; c < DC_NUM_COUNTERS; ++c)
         r[cnames[static_cast<size_t>(c)]] = static_cast<unsigned long long>(g->deltaSum[c]);
-      r["tensorcore_active"] = g->derivedSum[DD_MFMA_UTIL_PCT] / n;
+      r["tensorcore_active"] = g->derivedSum[DD_MFMA_UTIL_PCT] / n / 100.0;  // DCGM 1004: a ratio
       r["graphics_engine_active_ratio"] = g->derivedSum[DD_GPU_BUSY_PCT] / n / 100.0;
     }
     g->samples = g->failures = 0;

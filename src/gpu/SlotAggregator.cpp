@@ -103,7 +103,7 @@ void SlotAggregator::logInterval(Logger& logger, double sec) {
     for (int d = 0; d < DD_NUM_DERIVED; ++d)
       logger.logFloat(names[static_cast<size_t>(d)], static_cast<float>(a.derivedSum[d] / n));
     // reference-compatible aliases
-    logger.logFloat("tensorcore_active", static_cast<float>(a.derivedSum[DD_MFMA_UTIL_PCT] / n));
+    logger.logFloat("tensorcore_active", static_cast<float>(a.derivedSum[DD_MFMA_UTIL_PCT] / n / 100.0));  // DCGM 1004: a ratio
     logger.logFloat("sm_active_ratio", static_cast<float>(a.derivedSum[DD_SQ_BUSY_PCT] / n / 100.0));
     logger.logFloat("sm_occupancy", static_cast<float>(a.derivedSum[DD_OCCUPANCY_PCT] / n / 100.0));
     logger.logFloat("graphics_engine_active_ratio",

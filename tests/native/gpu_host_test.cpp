@@ -95,7 +95,8 @@ TEST(GpuHost, WorldEightGatherAggregatesPerRankAndPhase) {
     EXPECT_NEAR(num(rec, "counter_sample_rate_hz"), counts[static_cast<size_t>(r)] / 0.5, 1e-3);
     EXPECT_NEAR(num(rec, "gpu_busy_pct"), 10.0 * r, 1e-3);
     EXPECT_NEAR(num(rec, "graphics_engine_active_ratio"), 0.1 * r, 1e-3);
-    EXPECT_NEAR(num(rec, "tensorcore_active"), 40.0, 1e-3);
+    EXPECT_NEAR(num(rec, "mfma_util"), 40.0, 1e-3);
+    EXPECT_NEAR(num(rec, "tensorcore_active"), 0.40, 1e-5);  // the reference key is a ratio
     EXPECT_NEAR(num(rec, "sample_latency_us"), 2.0, 1e-3);
     EXPECT_NEAR(num(rec, "SQ_WAVES"), double(r + 1) * counts[static_cast<size_t>(r)], 0);
     EXPECT_FALSE(rec.contains("phase"));  // no phase names yet
