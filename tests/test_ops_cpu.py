@@ -63,3 +63,22 @@ def test_weight_transpose_registry_invalidation():
     assert ops._WT[ptr][0]() is None  # freed weight: its entry can no longer match
     ops.unregister_transposed(torch.empty(0))  # unknown pointer: no-op
     assert ops.dgrad_weights(llama.build_llama("tiny", device="cpu", dtype=torch.float32)) != []
+
+
+def test_activation_transpose_slot_offer_take():
+    """ops.offer_transposed / take_transposed: one slot, served once to a 2-D
+    view of the same storage, refused after a write or for another tensor,
+    replaced by the next offer."""
+    x = torch.randn(8, 6)
+    xt = x.t().contiguous()
+    ops.offer_transposed(x, xt)
+    assert ops.take_transposed(torch.randn(8, 6)) is None  # another tensor
+    assert ops.take_transposed(x.view(2, 4, 6).reshape(-1, 6)) is xt  # a view of it: served
+    assert ops.take_transposed(x) is None  # served once
+    ops.offer_transposed(x, xt)
+    x.add_(1.0)
+    assert ops.take_transposed(x) is None  # written since the offer
+    y = torch.randn(4, 4)
+    ops.offer_transposed(y, y.t().contiguous())
+    assert ops._ACT_T[0][0][0] == y.data_ptr()  # one slot: the newest offer
+    assert ops.take_transposed(y) is not None and ops._ACT_T[0] is None
