@@ -1,0 +1,6 @@
+# end-of-session check of the tree as committed (after reverting the RoPE experiment): op + attention tests, smoke, headline bench
+set -o pipefail
+O=gpurun_out/g47; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_ops_gpu.py tests/test_attention_gpu.py -x -v --timeout 120 --timeout-method thread > $O/pytest_ops.log 2>&1 && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+timeout -k 10 600 python -u bench.py --json-out $O/bench.json > $O/bench_headline.log 2>&1
