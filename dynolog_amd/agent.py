@@ -38,6 +38,43 @@ def _err(lib) -> str:
     return e.decode() if e else "unknown error"
 
 
+_VISIBLE_VARS = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
+def _index_list(v: str) -> Optional[List[int]]:
+    out = []
+    for tok in v.split(","):
+        tok = tok.strip()
+        if not tok:
+            continue
+        if not tok.isdigit():
+            return None  # UUIDs ("GPU-...") cannot be mapped without the runtime
+        out.append(int(tok))
+    return out
+
+
+def agent_index_for_local_rank(local_rank: int, environ=None) -> Optional[int]:
+    """rocprofiler-sdk GPU agent index of HIP device ``local_rank``.
+
+    The agents are the HSA devices, which ``ROCR_VISIBLE_DEVICES`` already
+    filters; ``HIP_VISIBLE_DEVICES`` (or, when unset, ``CUDA_VISIBLE_DEVICES``)
+    then selects and orders HIP devices by index INTO that HSA list.  So HIP
+    device d is agent ``hip_list[d]``, or agent d when no HIP list is set.
+    Returns None when it cannot be known without initialising the runtime
+    (a UUID list, or a local rank beyond the list): the caller then lets
+    preinit() create a counting context for every GPU."""
+    env = os.environ if environ is None else environ
+    for var in _VISIBLE_VARS:
+        v = env.get(var)
+        if v is None or v == "":
+            continue
+        lst = _index_list(v)
+        if lst is None or local_rank >= len(lst):
+            return None
+        return lst[local_rank]
+    return local_rank
+
+
 def preinit(agents: Optional[Sequence[int]] = None, kernel_trace: bool = False) -> None:
     """Register the rocprofiler-sdk tool. Must run before the HIP runtime
     initialises in this process (i.e. before the first torch.cuda call).

@@ -38,7 +38,7 @@ STAGE_META_DTYPE = np.dtype([("host_ts_ns", "<u8"), ("latency_ns", "<u4"), ("n_r
 
 GATHER_HEADER_DTYPE = np.dtype([
     ("first_seq", "<u8"), ("count", "<u4"), ("rank", "<u4"), ("dropped", "<u8"),
-    ("head", "<u8"), ("reserved", "<u8", (4,)),
+    ("head", "<u8"), ("backlog", "<u8"), ("cap", "<u4"), ("device", "<i4"), ("reserved", "<u8", (2,)),
 ])
 assert GATHER_HEADER_DTYPE.itemsize == 64
 
@@ -106,6 +106,32 @@ def reference_pack(raw: np.ndarray, ts_ns: np.ndarray, counter_of: np.ndarray,
         derived[b, D["sclk_mhz"]] = div(cnt, dt_us)
         derived[b, D["sample_dt_us"]] = dt_us
     return deltas, derived, flags
+
+
+def plan_gather_range(head: int, gathered: int, cap: int, ring_capacity: int):
+    """Mirror of planGatherRange (src/gpu/GatherPlan.h): (first, count, dropped, backlog).
+    Oldest pending slots first, at most cap; pending slots more than half the
+    ring behind the head are dropped."""
+    window = max(ring_capacity // 2, 1)
+    frm, dropped = gathered, 0
+    if head - frm > window:
+        dropped = head - frm - window
+        frm = head - window
+    count = min(head - frm, cap)
+    return frm, count, dropped, head - frm - count
+
+
+def parse_compact_drain(buf: bytes | np.ndarray, world: int):
+    """Split rank 0's compacted drain (world headers, then every rank's slots
+    back to back) into [(header, slots)] per rank."""
+    arr = np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+    hdrs = arr[:64 * world].view(GATHER_HEADER_DTYPE)
+    out, off = [], 64 * world
+    for r in range(world):
+        n = int(hdrs[r]["count"])
+        out.append((hdrs[r], arr[off:off + n * SLOT_BYTES].view(SLOT_DTYPE)))
+        off += n * SLOT_BYTES
+    return out
 
 
 def parse_gather_payload(buf: bytes | np.ndarray, cap_slots: int):

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "common/Json.h"
+#include "gpu/GatherPlan.h"
 #include "gpu/RocprofSampler.h"
 #include "gpu/SlotAggregator.h"
 #include "gpu/SlotFormat.h"
@@ -54,7 +55,9 @@ struct AgentConfig {
   int stages = 64;                   // pinned staging batches in flight (<= 256)
   bool forceCollective = false;      // testing: use the RCCL path (1-rank comm) at world 1
   uint64_t ringSlots = 1ull << 20;   // 256 MiB of HBM history per GPU
-  uint32_t gatherCapSlots = 4096;    // max slots per rank per gather (1 MiB)
+  uint32_t gatherCapSlots = 4096;    // max slots per rank per gather (1 MiB); the
+                                     // collective path agrees a smaller size each step
+                                     // from the ranks' pending counts (GatherPlan.h)
   std::string gatherMode = "gather"; // gather | allgather | shm (node-local mailbox) | none
   std::string counterSet = "lite";   // full | lite | core | comma list (RocprofSampler.h)
   int logIntervalMs = 1000;
@@ -182,11 +185,33 @@ class Agent {
   uint64_t prevTs_ = 0;
   int carryIdx_ = 0;
   std::mutex packMu_;
-  hipEvent_t packEvents_[8] = {};
-  int packEventNext_ = 0;
-  hipEvent_t lastPack_ = nullptr;
-  uint64_t lastPackHead_ = 0;   // ring head once lastPack_ completes (packMu_)
+  // One event per pack launch with the ring head it completes.  step()
+  // gathers through the newest mark whose event has COMPLETED (host query),
+  // so the trainer's stream never waits on the low-priority pack stream.
+  struct PackMark {
+    hipEvent_t ev = nullptr;
+    uint64_t head = 0;
+    bool used = false;
+  };
+  static constexpr int kPackMarks = 16;
+  PackMark packMarks_[kPackMarks];
+  int packMarkNext_ = 0;
+  uint64_t completedPackHead();  // newest completed mark's head (packMu_)
   uint64_t gatheredHost_ = 0;   // slots already handed to a gather (stepMu_)
+
+  // Collective payload sizing (GatherPlan.h): each gather max-reduces the
+  // ranks' pending counts into dAgree_[kAgree + e]; the drain stream copies it
+  // to hAgree_[e]; gather g + lag is sized from it.
+  static constexpr int kAgree = 8;
+  GatherSizer sizer_;
+  uint64_t* dAgree_ = nullptr;     // [kAgree] send, [kAgree] reduced
+  uint64_t* hAgree_ = nullptr;     // pinned [kAgree]
+  hipEvent_t agreeDone_[kAgree] = {};
+  uint64_t collectiveGathers_ = 0;  // gathers issued through RCCL (stepMu_)
+  uint32_t recvCap_[kRecv] = {};        // payload cap of the gather in each recv buffer
+  std::atomic<uint64_t> gatherBytes_{0}, gatherSlots_{0}, drainBytes_{0}, runAheadWaits_{0};
+  std::atomic<uint64_t> backlogNow_{0}, capNow_{0};
+  bool gatherCollective(hipStream_t stream, uint64_t head, std::string* err);
 
   ncclComm_t comm_ = nullptr;
   // gather_mode "shm" (world > 1, one node): ranks > 0 publish their payload

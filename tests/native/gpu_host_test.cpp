@@ -13,6 +13,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include "gpu/GatherPlan.h"
 #include "gpu/KernelCounters.h"
 #include "gpu/ShmGather.h"
 #include "gpu/SlotAggregator.h"
@@ -39,6 +40,7 @@ std::vector<uint8_t> makeGather(int world, uint32_t cap, uint64_t seqBase, bool 
     counts->push_back(std::min(n, cap));
     h->count = n;
     h->rank = static_cast<uint32_t>(r);
+    h->device = 10 + r;
     h->dropped = static_cast<uint64_t>(r);
     h->first_seq = seqBase;
     for (uint32_t i = 0; i < std::min(n, cap); ++i) {
@@ -90,9 +92,13 @@ TEST(GpuHost, WorldEightGatherAggregatesPerRankAndPhase) {
   ASSERT_EQ(store->records.size(), static_cast<size_t>(world));
   for (int r = 0; r < world; ++r) {
     const Json& rec = store->records[static_cast<size_t>(r)];
-    EXPECT_EQ(static_cast<int>(num(rec, "device")), r);
+    EXPECT_EQ(static_cast<int>(num(rec, "device")), 10 + r);  // the GPU id from the headers
+    EXPECT_EQ(static_cast<int>(num(rec, "rank")), r);
     EXPECT_NEAR(num(rec, "counter_samples"), counts[static_cast<size_t>(r)], 0);
-    EXPECT_NEAR(num(rec, "counter_sample_rate_hz"), counts[static_cast<size_t>(r)] / 0.5, 1e-3);
+    // rate over the slots' own window (10 ns apart here); one slot alone
+    // falls back to the logging interval
+    const double rate = counts[static_cast<size_t>(r)] > 1 ? 1e8 : counts[static_cast<size_t>(r)] / 0.5;
+    EXPECT_NEAR(num(rec, "counter_sample_rate_hz") / rate, 1.0, 1e-3);
     EXPECT_NEAR(num(rec, "gpu_busy_pct"), 10.0 * r, 1e-3);
     EXPECT_NEAR(num(rec, "graphics_engine_active_ratio"), 0.1 * r, 1e-3);
     EXPECT_NEAR(num(rec, "mfma_util"), 40.0, 1e-3);
@@ -331,4 +337,139 @@ TEST(GpuHost, KernelCountersPoolRareClasses) {
   EXPECT_LE(std::fabs(r.classes[0].rate[KC_TFLOPS] - 1200.0), 20.0);
   EXPECT_LE(std::fabs(r.classes[1].rate[KC_HBM_WRITE] - 3000.0), 50.0);
   EXPECT_GT(r.classes[2].kernelNs, 0.0);
+}
+
+// Per-step gather sizing on a synthetic 8-rank run (GatherPlan.h): every
+// rank produces ~336 slots per step (1 kHz at a 336 ms step), one rank has a
+// 3000-slot burst.  Each rank sizes its payload from the max-reduced need of
+// the gather `lag` steps earlier, exactly as Agent::gatherCollective does.
+// The xGMI bytes per step must track the new slots (not the 1 MiB worst
+// case), every slot must arrive in order, none may be dropped, and the
+// burst must drain within a few steps.
+TEST(GatherPlan, EightRankScheduleBytesTrackNewSlots) {
+  const int world = 8, steps = 400;
+  const uint64_t ring = 1ull << 20;
+  GatherSizer sizer(4096, GatherSizer::kQuantum, GatherSizer::kDefaultLag);
+  std::vector<uint64_t> produced(world, 0), head(world, 0), gathered(world, 0), nextSeq(world, 0), dropped(world, 0);
+  std::vector<uint64_t> agreed;  // max need per gather
+  uint32_t lcg = 777;
+  uint64_t newSlots = 0, sentBytes = 0, sentSlots = 0, fixedBytes = 0;
+  uint64_t newAfterWarm = 0, bytesAfterWarm = 0;
+  int burstDrainedAt = -1;
+  for (int g = 0; g < steps; ++g) {
+    uint64_t stepNew = 0;
+    for (int r = 0; r < world; ++r) {
+      lcg = lcg * 1664525u + 1013904223u;
+      uint64_t n = 328 + (lcg >> 8) % 17;  // 328..344
+      if (g == 200 && r == 3) n += 3000;   // a stall on one rank, then a burst
+      // step() sees only completed packs of 32 samples
+      produced[static_cast<size_t>(r)] += n;
+      const uint64_t h = produced[static_cast<size_t>(r)] / 32 * 32;
+      stepNew += h - head[static_cast<size_t>(r)];
+      head[static_cast<size_t>(r)] = h;
+    }
+    newSlots += stepNew;
+    const uint32_t cap = sizer.capFor(static_cast<uint64_t>(g), g >= 4 ? agreed[static_cast<size_t>(g - 4)] : 0);
+    uint64_t maxNeed = 0, backlog = 0;
+    for (int r = 0; r < world; ++r) {
+      const size_t i = static_cast<size_t>(r);
+      maxNeed = std::max(maxNeed, head[i] - gathered[i]);
+      const auto rg = planGatherRange(head[i], gathered[i], cap, ring);
+      EXPECT_EQ(rg.first, nextSeq[i]);  // in order, nothing skipped
+      nextSeq[i] = rg.first + rg.count;
+      gathered[i] = rg.first + rg.count;
+      dropped[i] += rg.dropped;
+      backlog += rg.backlog;
+      sentSlots += rg.count;
+    }
+    agreed.push_back(maxNeed);
+    sentBytes += world * gatherBlockBytes(cap);
+    fixedBytes += world * gatherBlockBytes(4096);
+    if (g >= 20 && (g < 195 || g > 215)) {
+      newAfterWarm += stepNew;
+      bytesAfterWarm += world * gatherBlockBytes(cap);
+    }
+    if (g > 200 && burstDrainedAt < 0 && backlog == 0) burstDrainedAt = g;
+  }
+  for (int r = 0; r < world; ++r) EXPECT_EQ(dropped[static_cast<size_t>(r)], 0u);
+  EXPECT_GT(burstDrainedAt, 200);
+  EXPECT_LE(burstDrainedAt, 212);  // 3000 extra slots spread over a few steps
+  // steady state: payload bytes within 1.35x of the new slots' bytes
+  const double ratio = static_cast<double>(bytesAfterWarm) / (static_cast<double>(newAfterWarm) * sizeof(DynoSlot));
+  printf("gather bytes / new-slot bytes (steady state): %.3f; vs fixed 1 MiB payload: %.4f\n", ratio,
+         static_cast<double>(sentBytes) / static_cast<double>(fixedBytes));
+  EXPECT_LT(ratio, 1.35);
+  EXPECT_GT(ratio, 1.0);
+  // ...and far below the fixed worst-case payload (12x in round 2)
+  EXPECT_LT(static_cast<double>(sentBytes) / static_cast<double>(fixedBytes), 0.15);
+  EXPECT_LE(sentSlots, newSlots);
+  EXPECT_GE(sentSlots + 8 * 400, newSlots);  // all but the last step's remainder delivered
+}
+
+// Rank 0's drain: the compacted layout (headers + real slots only) folded by
+// SlotAggregator::ingestCompact, and its byte count.
+TEST(GatherPlan, CompactDrainIngest) {
+  const int world = 8;
+  const uint32_t cap = 64;
+  std::vector<uint32_t> counts;
+  auto buf = makeGather(world, cap, 0, false, &counts);
+  std::vector<uint8_t> out(buf.size(), 0);
+  const size_t bytes = compactGather(buf.data(), SlotAggregator::blockBytes(cap), world, cap, out.data());
+  uint64_t total = 0;
+  for (auto c : counts) total += c;
+  EXPECT_EQ(bytes, world * sizeof(DynoGatherHeader) + total * sizeof(DynoSlot));
+  EXPECT_LT(bytes, buf.size() / 3);  // 8 blocks of 64 slots mostly empty
+  SlotAggregator agg;
+  agg.reset(world, cap);
+  std::vector<std::pair<uint32_t, uint64_t>> seen;
+  EXPECT_EQ(agg.ingestCompact(out.data(), world, [&](const DynoSlot& s) { seen.emplace_back(s.rank, s.seq); }),
+            total);
+  EXPECT_EQ(seen.size(), static_cast<size_t>(total));
+  for (int r = 0; r < world; ++r) {
+    EXPECT_EQ(agg.rank(r).samples, counts[static_cast<size_t>(r)]);
+    EXPECT_EQ(agg.rank(r).device, 10 + r);
+    EXPECT_EQ(agg.rank(r).lastSeq, counts[static_cast<size_t>(r)] - 1u);
+  }
+}
+
+// Slots reach rank 0 in bursts (one gather per 336 ms training step) while
+// the sampler runs at 1 kHz: the interval record must report 1000 Hz, and be
+// stamped at its samples' window end, not at log time.
+TEST(GpuHost, IntervalRateFromSlotWindowUnderBurstyIngest) {
+  SlotAggregator agg;
+  agg.reset(1, 4096);
+  auto store = std::make_shared<MemoryLogger::Store>();
+  MemoryLogger ml(store);
+  const uint64_t t0 = 5'000'000'000ull;
+  uint64_t seq = 0;
+  std::vector<DynoSlot> slots(336);
+  auto deliver = [&]() {
+    for (auto& s : slots) {
+      s = DynoSlot{};
+      s.seq = seq;
+      s.host_ts_ns = t0 + seq * 1'000'000ull;  // 1 ms apart
+      ++seq;
+    }
+    DynoGatherHeader h{};
+    h.count = static_cast<uint32_t>(slots.size());
+    h.device = 5;
+    agg.ingestRank(0, h, slots.data());
+  };
+  // interval 1: 3 steps delivered, logged 0.7 s after the last sample
+  for (int i = 0; i < 3; ++i) deliver();
+  const uint64_t lastTs = t0 + (seq - 1) * 1'000'000ull;
+  const auto before = std::chrono::system_clock::now();
+  agg.logInterval(ml, 1.7, lastTs + 700'000'000ull);
+  // interval 2: one step, after a logging interval of 0.3 s
+  deliver();
+  agg.logInterval(ml, 0.3, t0 + (seq - 1) * 1'000'000ull + 10'000'000ull);
+  ASSERT_EQ(store->records.size(), 2u);
+  EXPECT_NEAR(num(store->records[0], "counter_sample_rate_hz"), 1000.0, 1.0);
+  EXPECT_NEAR(num(store->records[1], "counter_sample_rate_hz"), 1000.0, 1.0);
+  EXPECT_EQ(static_cast<int>(num(store->records[0], "device")), 5);
+  EXPECT_EQ(static_cast<int>(num(store->records[0], "rank")), 0);
+  // stamped ~0.7 s before the logging call (the last sample's time)
+  const double ageMs = std::chrono::duration<double, std::milli>(before - std::chrono::system_clock::time_point(
+      std::chrono::milliseconds(store->records[0].at("ts_ms").asInt()))).count();
+  EXPECT_NEAR(ageMs, 700.0, 50.0);
 }

@@ -137,3 +137,22 @@ def test_window_counts_per_rank_windows():
     a = agent.GpuAgent(_Lib(), {"rank": 0, "world": 2})
     assert a.window_counts(15, 35) == [2, 0]                   # one window: rank 1 misses
     assert a.window_counts([15, 1015], [35, 1035]) == [2, 2]   # its own window: counted
+
+
+@pytest.mark.parametrize("env,local_rank,want", [
+    ({}, 3, 3),                                               # every GPU visible
+    ({"HIP_VISIBLE_DEVICES": "4,5,6,7"}, 1, 5),               # second GPU of the upper half
+    ({"CUDA_VISIBLE_DEVICES": "7,2"}, 0, 7),                  # order follows the list
+    ({"HIP_VISIBLE_DEVICES": "1", "CUDA_VISIBLE_DEVICES": "6"}, 0, 1),  # HIP wins
+    ({"ROCR_VISIBLE_DEVICES": "2,3"}, 1, 1),                  # agents are already filtered
+    ({"ROCR_VISIBLE_DEVICES": "2,3,4", "HIP_VISIBLE_DEVICES": "2"}, 0, 2),
+    ({"HIP_VISIBLE_DEVICES": "GPU-1f2e3d4c5b6a7988"}, 0, None),  # UUID: unknown
+    ({"HIP_VISIBLE_DEVICES": "0,1"}, 2, None),                # rank beyond the list
+    ({"HIP_VISIBLE_DEVICES": ""}, 2, 2),                      # empty = unset
+])
+def test_agent_index_for_local_rank(env, local_rank, want):
+    """Each rank creates exactly one rocprofiler counting context: its
+    LOCAL_RANK (a HIP device index) is mapped to the agent through the
+    visible-devices lists (bench.py calls this before HIP initialises)."""
+    from dynolog_amd.agent import agent_index_for_local_rank
+    assert agent_index_for_local_rank(local_rank, env) == want

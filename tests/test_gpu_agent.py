@@ -334,6 +334,15 @@ def test_rccl_gather_path_with_one_rank(native_built, mode):
     assert st["last_error"] == "" and not st["gather_failed"], st
     assert st["gathers"] >= 40, st
     assert res["wc"][0] > 0 and st["ranks"][0]["received"] >= res["wc"][0], st
+    # rank 0 drains only the headers + the slots that were sent (compaction
+    # kernel), not the payload capacity
+    assert st["drain_bytes"] == 64 * st["gathers"] + 256 * st["ranks"][0]["received"], st
+    assert st["gather_slots"] == st["ranks"][0]["received"], st
+    # after the first `lag` gathers the payload follows the agreed need
+    # (a few slots per step here), far below the 4096-slot maximum
+    full = 64 + 4096 * 256
+    assert st["gather_bytes"] < 4 * full + (st["gathers"] - 4) * 0.1 * full, st
+    assert st["gather_cap_slots_now"] < 4096, st
 
 
 def test_agent_restart_returns_device_memory(native_built):

@@ -7,7 +7,7 @@ import pytest
 
 SUITES = ["Json", "Flags", "System", "KernelCollector", "Sinks", "SmiMonitor", "Rpc",
           "KinetoConfigManager", "IpcFabric", "IpcMonitor", "Pmu", "MetricFrame",
-          "RingBuffer", "TagStack", "PerfSampling", "Mon", "GpuHost"]
+          "RingBuffer", "TagStack", "PerfSampling", "Mon", "GpuHost", "GatherPlan"]
 
 
 @pytest.mark.parametrize("suite", SUITES)
