@@ -96,6 +96,16 @@ void RpcServer::stop() {
   for (auto& t : pool_)
     if (t.joinable()) t.join();
   pool_.clear();
+  {
+    // long calls finish their work (a trace ends by its own duration)
+    std::vector<LongCall> ts;
+    {
+      std::lock_guard<std::mutex> g(longMu_);
+      ts.swap(longCalls_);
+    }
+    for (auto& t : ts)
+      if (t.th.joinable()) t.th.join();
+  }
   std::lock_guard<std::mutex> g(mu_);
   for (int c : pending_) ::close(c);
   pending_.clear();
@@ -141,34 +151,71 @@ bool RpcServer::processOne(int acceptTimeoutMs) {
   return true;
 }
 
-void RpcServer::handleClient(int c) {
+bool RpcServer::readRequest(int c, std::string* msg) {
   net::setIoTimeout(c, ioTimeoutMs_);
   int32_t len = -1;
-  std::string msg;
   if (net::recvAll(c, &len, sizeof(len)) && len > 0 && len <= kMaxMessage) {
-    msg.resize(static_cast<size_t>(len));
-    if (!net::recvAll(c, msg.data(), msg.size())) {
+    msg->resize(static_cast<size_t>(len));
+    if (!net::recvAll(c, msg->data(), msg->size())) {
       LOG(ERROR) << "Unexpected message size, expected " << len;
-      msg.clear();
+      msg->clear();
     }
   } else {
     LOG(ERROR) << "Failed to read message size (" << len << ")";
   }
-  if (!msg.empty()) {
-    std::string resp;
-    try {
-      resp = dispatcher_->processOne(msg);
-    } catch (const std::exception& e) {
-      LOG(ERROR) << "RPC handler threw: " << e.what();
-    }
-    if (!resp.empty()) {
-      int32_t rl = static_cast<int32_t>(resp.size());
-      if (!net::sendAll(c, &rl, sizeof(rl)) || !net::sendAll(c, resp.data(), resp.size()))
-        LOG(ERROR) << "Failed to send response";
-    }
+  return !msg->empty();
+}
+
+void RpcServer::reply(int c, const std::string& msg) {
+  std::string resp;
+  try {
+    resp = dispatcher_->processOne(msg);
+  } catch (const std::exception& e) {
+    LOG(ERROR) << "RPC handler threw: " << e.what();
+  }
+  if (!resp.empty()) {
+    int32_t rl = static_cast<int32_t>(resp.size());
+    if (!net::sendAll(c, &rl, sizeof(rl)) || !net::sendAll(c, resp.data(), resp.size()))
+      LOG(ERROR) << "Failed to send response";
   }
   ::close(c);
   served_++;
+}
+
+void RpcServer::handleClient(int c) {
+  std::string msg;
+  if (!readRequest(c, &msg)) {
+    ::close(c);
+    served_++;
+    return;
+  }
+  // long calls (traces) get a thread of their own; the pool worker returns
+  Json req = parseRequest(msg);
+  if (!req.isNull() && req.at("fn").isString() && dispatcher_->isLong(req.at("fn").asString())) {
+    std::lock_guard<std::mutex> g(longMu_);
+    // reap the calls that have finished (join returns at once)
+    for (auto it = longCalls_.begin(); it != longCalls_.end();) {
+      if (it->done->load()) {
+        it->th.join();
+        it = longCalls_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    if (longInFlight_ < kMaxLongInFlight) {
+      longInFlight_++;
+      auto done = std::make_shared<std::atomic<bool>>(false);
+      longCalls_.push_back({std::thread([this, c, msg, done] {
+                              reply(c, msg);
+                              longInFlight_--;
+                              *done = true;
+                            }),
+                            done});
+      return;
+    }
+    LOG(WARNING) << "RPC: " << kMaxLongInFlight << " long calls in flight, serving inline";
+  }
+  reply(c, msg);
 }
 
 bool rpcCall(const std::string& host, int port, const std::string& request, std::string* response,

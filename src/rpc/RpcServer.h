@@ -20,6 +20,7 @@
 #include <memory>
 #include <mutex>
 #include <optional>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -34,12 +35,20 @@ using RpcFn = std::function<std::optional<Json>(const Json& request)>;
 class RpcDispatcher {
  public:
   void add(const std::string& fn, RpcFn f) { fns_[fn] = std::move(f); }
+  // A call that may take seconds (traces): the server serves its connection
+  // on a thread of its own so the worker pool stays free (rpc/Jobs.h).
+  void addLong(const std::string& fn, RpcFn f) {
+    fns_[fn] = std::move(f);
+    long_.insert(fn);
+  }
+  bool isLong(const std::string& fn) const { return long_.count(fn) > 0; }
   // Full request string -> response string ("" = no reply).
   std::string processOne(const std::string& request) const;
   std::vector<std::string> functions() const;
 
  private:
   std::map<std::string, RpcFn> fns_;
+  std::set<std::string> long_;
 };
 
 // Validates like the reference's toJson(): object with "fn", else null Json.
@@ -59,14 +68,19 @@ class RpcServer {
   // processOne() semantics). Returns false if accept timed out.
   bool processOne(int acceptTimeoutMs = 5000);
   uint64_t served() const { return served_; }
+  int longInFlight() const { return longInFlight_; }
 
   static constexpr int kBacklog = 50;
+  static constexpr int kMaxLongInFlight = 16;
   static constexpr int32_t kMaxMessage = 16 << 20;
 
  private:
   void acceptLoop();
   void workerLoop();
   void handleClient(int cfd);
+  // reads one framed request; false (connection to close) if there is none
+  bool readRequest(int cfd, std::string* msg);
+  void reply(int cfd, const std::string& msg);
 
   std::shared_ptr<RpcDispatcher> dispatcher_;
   int fd_ = -1;
@@ -81,6 +95,13 @@ class RpcServer {
   std::condition_variable cv_;
   std::deque<int> pending_;
   std::atomic<uint64_t> served_{0};
+  std::mutex longMu_;
+  struct LongCall {
+    std::thread th;
+    std::shared_ptr<std::atomic<bool>> done;
+  };
+  std::vector<LongCall> longCalls_;
+  std::atomic<int> longInFlight_{0};
 };
 
 // Blocking client: one request/response over a fresh connection.
