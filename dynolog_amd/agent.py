@@ -220,7 +220,7 @@ class GpuAgent:
               log_file: str = "", uid: Optional[bytes] = None, process_group=None,
               daemon_endpoint: str = "dynolog", fault_inject: str = "",
               slot_ring: str = "", stages: int = 64,
-              force_collective: bool = False) -> "GpuAgent":
+              force_collective: bool = False, counter_passes: str = "") -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
@@ -233,7 +233,12 @@ class GpuAgent:
         ``sinks``: any of "json" (daemon-format log lines), "memory" (queryable
         via memory_records()), "prometheus", "daemon" (forward every per-GPU
         record to the node's dynolog daemon over the IPC fabric as a "gmet"
-        message; needs ``dynolog --enable_ipc_monitor``)."""
+        message; needs ``dynolog --enable_ipc_monitor``).
+
+        ``counter_passes``: rotate counter configs per pack batch, e.g.
+        ``"lite:3,precision:1"`` (3 batches of the lite set, then 1 of the
+        precision set: per-precision VALU FLOPs -> fp16/32/64_active, MFMA
+        MOPs by type, VALU busy).  Empty: one pass of ``counter_set``."""
         if not _preinit_done:
             raise AgentError("dynolog_amd.agent.preinit() must be called before HIP init")
         lib = _native.load_gpu_lib()
@@ -252,6 +257,8 @@ class GpuAgent:
                    ring_slots=ring_slots, gather_cap_slots=gather_cap_slots,
                    gather_mode=gather_mode, counter_set=counter_set, log_interval_ms=log_interval_ms,
                    sinks=list(sinks), log_file=log_file, daemon_endpoint=daemon_endpoint)
+        if counter_passes:
+            cfg["counter_passes"] = counter_passes
         if force_collective:  # testing: RCCL gather path with a 1-rank communicator
             cfg["force_collective"] = True
         if fault_inject:  # testing: "gather_error@N"
@@ -285,7 +292,8 @@ class GpuAgent:
                                   gather_mode=fallback, counter_set=counter_set,
                                   log_interval_ms=log_interval_ms, sinks=sinks, log_file=log_file,
                                   process_group=process_group, daemon_endpoint=daemon_endpoint,
-                                  fault_inject=fault_inject, slot_ring=slot_ring, stages=stages)
+                                  fault_inject=fault_inject, slot_ring=slot_ring, stages=stages,
+                                  counter_passes=counter_passes)
                 # report the mode that was asked for; a chained fallback (RCCL,
                 # then the mailbox) keeps every reason, first failure first
                 inner = agent.config.get("fallback_reason")

@@ -60,6 +60,8 @@ struct AgentConfig {
                                      // from the ranks' pending counts (GatherPlan.h)
   std::string gatherMode = "gather"; // gather | allgather | shm (node-local mailbox) | none
   std::string counterSet = "lite";   // full | lite | core | comma list (RocprofSampler.h)
+  std::string counterPasses;         // "" = one pass of counterSet; "lite:3,precision:1"
+                                     // rotates counter configs per pack batch
   int logIntervalMs = 1000;
   std::vector<std::string> sinks = {"json"};  // json | memory | prometheus | daemon | none
   std::string daemonEndpoint = "dynolog";     // IPC endpoint of the node daemon ("daemon" sink)
@@ -122,15 +124,30 @@ class Agent {
   bool flushBatch(int nstaged, std::string* err);
   void consumerLoop();
   void logInterval();
-  bool setupLayout(const std::vector<uint64_t>& ids, std::string* err);
+  struct PassState {
+    CounterPassSpec spec;
+    std::unique_ptr<CounterSampler> sampler;
+    DynoAgentConsts consts{};
+    size_t R = 0;  // raw instance values per sample
+    int* dPerm = nullptr;
+    int* dSegStart = nullptr;
+    int* dSegLen = nullptr;
+  };
+  bool setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::string* err);
+  void switchPass();  // sampler thread: stop the current pass, start the next
   void releaseDevice();
   void waitSamplesThrough(uint64_t t1) const;  // rank 0: samples up to t1 ingested (<= 1 s)
   std::unique_ptr<Logger> makeLogger();
 
   AgentConfig cfg_;
-  std::unique_ptr<CounterSampler> sampler_;
-  std::vector<std::string> counterNames_;
-  DynoAgentConsts consts_{};
+  std::vector<PassState> passes_;
+  int curPass_ = 0;                  // sampler thread
+  int batchesInPass_ = 0;
+  CounterSampler* sampler_ = nullptr;  // the current pass's sampler
+  bool zeroPrevNext_ = false;        // next pack: deltas vs zero from switchTs_ (fresh counters)
+  uint64_t switchTs_ = 0;
+  std::atomic<uint64_t> passSwitches_{0}, passSwitchNs_{0};
+  double* dZero_ = nullptr;
   std::atomic<bool> running_{false};
   std::atomic<bool> stopFlag_{false};
   std::atomic<bool> paused_{false};
@@ -151,9 +168,6 @@ class Agent {
   double* dStage_ = nullptr;
   DynoStageMeta* dMeta_ = nullptr;
   double* dCarry_[2] = {nullptr, nullptr};
-  int* dPerm_ = nullptr;
-  int* dSegStart_ = nullptr;
-  int* dSegLen_ = nullptr;
   uint8_t* dSend_ = nullptr;
   size_t sendBytes_ = 0;
   static constexpr int kRecv = 4;

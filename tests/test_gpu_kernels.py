@@ -38,7 +38,7 @@ def _layout(rng, counts):
 
 
 def _run_pack(lib, raw, ts, counter_of, perm, seg_start, seg_len, prev_raw, prev_ts,
-              base_seq=0, ring_slots=64, rank=3):
+              base_seq=0, ring_slots=64, rank=3, pass_id=S.PASS_MAIN):
     B, R = raw.shape
     meta = np.zeros(B, dtype=S.STAGE_META_DTYPE)
     meta["host_ts_ns"] = ts
@@ -55,7 +55,7 @@ def _run_pack(lib, raw, ts, counter_of, perm, seg_start, seg_len, prev_raw, prev
         _ptr(seg_start), _ptr(seg_len), len(seg_len),
         _ptr(prev_raw) if prev_raw is not None else None, ctypes.c_ulonglong(prev_ts),
         _ptr(consts), ctypes.c_ulonglong(base_seq), ctypes.c_ulonglong(ring_slots),
-        ctypes.c_uint(rank), _ptr(out), _ptr(carry), ctypes.byref(head))
+        ctypes.c_uint(rank), _ptr(out), _ptr(carry), ctypes.byref(head), ctypes.c_uint(pass_id))
     assert rc == 0, rc
     return out, carry, head.value
 
@@ -94,6 +94,48 @@ def test_pack_matches_reference(native_built, B, first):
     np.testing.assert_array_equal(carry, raw[-1])
     assert head == 40 + B
     assert (out["gpu_pack_ticks"] > 0).all()
+    np.testing.assert_array_equal(out["pass"], S.PASS_MAIN)
+
+
+def _precision_counts():
+    # precision pass positions: 8 SQ counters (per SE), 2 TCC (per channel), GRBM (per XCD)
+    counts = [0] * 14
+    for pos in range(8):
+        counts[pos] = 32
+    counts[S.P["TCC_EA0_RDREQ"]] = counts[S.P["TCC_EA0_WRREQ"]] = 128
+    counts[S.P["GRBM_GUI_ACTIVE"]] = counts[S.P["GRBM_COUNT"]] = 8
+    return counts
+
+
+@pytest.mark.parametrize("fresh", [False, True])
+def test_pack_precision_pass_matches_reference(native_built, fresh):
+    """The precision counter pass: fp16/32/64_active, VALU busy and the
+    shared busy / HBM / bf16 metrics vs the float64 reference.  `fresh` is the
+    first batch after a pass switch: previous sample = zeros at the switch time
+    (the counters restarted with the context)."""
+    lib = _lib(native_built)
+    rng = np.random.default_rng(11)
+    counts = _precision_counts()
+    counter_of, perm, seg_start, seg_len = _layout(rng, counts)
+    R = len(counter_of)
+    B = 16
+    base = np.zeros(R) if fresh else rng.integers(0, 2**40, size=R).astype(np.float64)
+    inc = rng.integers(0, 2**22, size=(B, R)).astype(np.float64)
+    raw = base + np.cumsum(inc, axis=0)
+    t0 = 9_000_000_000
+    ts = t0 + np.cumsum(rng.integers(900_000, 1_100_000, size=B)).astype(np.uint64)
+    out, carry, head = _run_pack(lib, raw, ts, counter_of, perm, seg_start, seg_len, base, t0,
+                                 base_seq=3, ring_slots=64, pass_id=S.PASS_PRECISION)
+    ref_d, ref_der, ref_flags = S.reference_pack(raw, ts.astype(np.int64), counter_of, base, t0,
+                                                 pass_id=S.PASS_PRECISION)
+    np.testing.assert_array_equal(out["pass"], S.PASS_PRECISION)
+    np.testing.assert_array_equal(out["flags"], ref_flags)
+    np.testing.assert_array_equal(out["delta"][:, :14], np.rint(ref_d[:, :14]).astype(np.uint64))
+    np.testing.assert_allclose(out["derived"], ref_der, rtol=2e-6, atol=1e-4)
+    # only the precision pass's metrics are set
+    for name in ("mfma_util", "occupancy_pct", "lds_bank_conflict_rate"):
+        assert (out["derived"][:, S.D[name]] == 0).all()
+    assert (out["derived"][:, S.D["fp32_active"]] > 0).all()
 
 
 def test_pack_counter_reset_flag(native_built):

@@ -65,8 +65,8 @@ __global__ __launch_bounds__(256) void k_fp64(double* out, int iters) {
   }
   if (a + c + d == 1234.5) out[threadIdx.x] = a;
 }
-__global__ __launch_bounds__(256) void k_fp16(float* out, int iters) {
-  half2_t a = {(_Float16)(threadIdx.x * 1e-3f), (_Float16)0.1f}, b = {(_Float16)1.0f, (_Float16)1.0f},
+__global__ __launch_bounds__(256) void k_fp16(float* out, int iters, float scale) {
+  half2_t a = {(_Float16)(threadIdx.x * 1e-3f), (_Float16)0.1f}, b = {(_Float16)scale, (_Float16)scale},
           c = {(_Float16)0.5f, (_Float16)0.25f};
   for (int i = 0; i < iters; ++i) {
     a = a * b + c;
@@ -215,13 +215,15 @@ int main(int argc, char** argv) {
   Cfg main_{"lite", {"SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES",
                      "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
                      "TCC_EA0_RDREQ", "TCC_EA0_WRREQ", "GRBM_GUI_ACTIVE", "GRBM_COUNT"}};
-  Cfg prec{"precision", {"SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32",
-                         "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_FMA_F16", "SQ_INSTS_VALU_FMA_F64",
-                         "SQ_INSTS_VALU_MFMA_MOPS_F32", "SQ_INSTS_VALU_MFMA_MOPS_F64", "TCC_EA0_RDREQ",
+  // the agent's precision pass, exactly
+  Cfg prec{"precision", {"SQ_INSTS_VALU_FLOPS_FP16", "SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP64",
+                         "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_VALU_MFMA_MOPS_F32",
+                         "SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_ACTIVE_INST_VALU", "TCC_EA0_RDREQ",
                          "TCC_EA0_WRREQ", "GRBM_GUI_ACTIVE", "GRBM_COUNT"}};
-  Cfg prec2{"precision2", {"SQ_INSTS_VALU_ADD_F16", "SQ_INSTS_VALU_MUL_F16", "SQ_INSTS_VALU_TRANS_F16",
-                           "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_TRANS_F64",
-                           "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE", "GRBM_COUNT"}};
+  // instruction counts to calibrate the FLOPS counters against
+  Cfg prec2{"precision2", {"SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_FMA_F16",
+                           "SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+                           "SQ_INSTS_VALU_FLOPS_FP32_TRANS", "SQ_ACTIVE_INST_VALU2", "GRBM_GUI_ACTIVE", "GRBM_COUNT"}};
   if (!build(main_)) return 1;
   const bool havePrec = build(prec);
   const bool havePrec2 = build(prec2);
@@ -285,7 +287,7 @@ int main(int argc, char** argv) {
   std::vector<W> ws = {
       {"fp32_valu", [&] { hipLaunchKernelGGL(k_fp32, dim3(4096), dim3(256), 0, s, outf, 20000); }},
       {"fp64_valu", [&] { hipLaunchKernelGGL(k_fp64, dim3(4096), dim3(256), 0, s, outd, 5000); }},
-      {"fp16_valu", [&] { hipLaunchKernelGGL(k_fp16, dim3(4096), dim3(256), 0, s, outf, 20000); }},
+      {"fp16_valu", [&] { hipLaunchKernelGGL(k_fp16, dim3(4096), dim3(256), 0, s, outf, 20000, 1.0001f); }},
       {"bf16_mfma", [&] { hipLaunchKernelGGL(k_mfma, dim3(4096), dim3(256), 0, s, outf, 20000); }},
   };
   for (auto& w : ws) {
@@ -300,7 +302,7 @@ int main(int argc, char** argv) {
       HC(hipStreamSynchronize(s));
       auto b = sample(cap, &n, &us);
       stopCtx();
-      fprintf(stderr, "[%s under %s]", c.name.c_str(), w.name);
+      fprintf(stderr, "[%s under %s] (lanes x iters = %.4g)", c.name.c_str(), w.name, 4096.0 * 256 * 20000);
       for (auto& [k, v] : b) fprintf(stderr, " %s=%.3g", k.c_str(), v - a[k]);
       fprintf(stderr, "\n");
     }
