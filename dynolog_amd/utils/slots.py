@@ -123,9 +123,10 @@ def reference_pack(raw: np.ndarray, ts_ns: np.ndarray, counter_of: np.ndarray,
         derived[b, D["sample_dt_us"]] = dt_us
         simd_cycles = gui * k["simd_count"]
         if pass_id == PASS_PRECISION:
-            derived[b, D["fp16_active"]] = div(s[P["SQ_INSTS_VALU_FLOPS_FP16"]], simd_cycles * k["valu_fp16_flops_per_clk"])
-            derived[b, D["fp32_active"]] = div(s[P["SQ_INSTS_VALU_FLOPS_FP32"]], simd_cycles * k["valu_fp32_flops_per_clk"])
-            derived[b, D["fp64_active"]] = div(s[P["SQ_INSTS_VALU_FLOPS_FP64"]], simd_cycles * k["valu_fp64_flops_per_clk"])
+            # the VALU FLOPS counters tally FLOPs per wave instruction: x64 lanes
+            derived[b, D["fp16_active"]] = div(64 * s[P["SQ_INSTS_VALU_FLOPS_FP16"]], simd_cycles * k["valu_fp16_flops_per_clk"])
+            derived[b, D["fp32_active"]] = div(64 * s[P["SQ_INSTS_VALU_FLOPS_FP32"]], simd_cycles * k["valu_fp32_flops_per_clk"])
+            derived[b, D["fp64_active"]] = div(64 * s[P["SQ_INSTS_VALU_FLOPS_FP64"]], simd_cycles * k["valu_fp64_flops_per_clk"])
             derived[b, D["valu_busy_pct"]] = 400 * div(s[P["SQ_ACTIVE_INST_VALU"]], simd_cycles)
             continue
         derived[b, D["mfma_util"]] = 100 * div(s[C["SQ_VALU_MFMA_BUSY_CYCLES"]], simd_cycles)

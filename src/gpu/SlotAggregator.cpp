@@ -196,9 +196,10 @@ void SlotAggregator::logInterval(Logger& logger, double sec, uint64_t monoNowNs)
       logger.logFloat("mfma_f16_tflops", tf(512.0 * static_cast<double>(pd[DP_MFMA_MOPS_F16])));
       logger.logFloat("mfma_f32_tflops", tf(512.0 * static_cast<double>(pd[DP_MFMA_MOPS_F32])));
       logger.logFloat("mfma_f64_tflops", tf(512.0 * static_cast<double>(pd[DP_MFMA_MOPS_F64])));
-      logger.logFloat("valu_fp16_tflops", tf(static_cast<double>(pd[DP_VALU_FLOPS_FP16])));
-      logger.logFloat("valu_fp32_tflops", tf(static_cast<double>(pd[DP_VALU_FLOPS_FP32])));
-      logger.logFloat("valu_fp64_tflops", tf(static_cast<double>(pd[DP_VALU_FLOPS_FP64])));
+      // the VALU FLOPS counters tally per wave instruction: x64 lanes
+      logger.logFloat("valu_fp16_tflops", tf(64.0 * static_cast<double>(pd[DP_VALU_FLOPS_FP16])));
+      logger.logFloat("valu_fp32_tflops", tf(64.0 * static_cast<double>(pd[DP_VALU_FLOPS_FP32])));
+      logger.logFloat("valu_fp64_tflops", tf(64.0 * static_cast<double>(pd[DP_VALU_FLOPS_FP64])));
     }
     logger.finalize();
     // per workload phase (markers), only once phases are in use

@@ -208,6 +208,16 @@ void RelayLogger::finalize() {
   clearSample();
 }
 
+// ---------------------------------------------------------- RecordLogger
+void RecordLogger::finalize() {
+  if (!rec_.asObject().empty()) {
+    rec_["ts_ms"] = static_cast<long long>(
+        std::chrono::duration_cast<std::chrono::milliseconds>(ts_.time_since_epoch()).count());
+    records.push_back(std::move(rec_));
+  }
+  rec_ = Json::object();
+}
+
 // ---------------------------------------------------------- MemoryLogger
 void MemoryLogger::finalize() {
   Json rec = sample();

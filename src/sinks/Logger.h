@@ -123,6 +123,25 @@ class RelayLogger : public JsonLogger {
   std::string hostname_;
 };
 
+// Collects finalized records as JSON objects with numbers kept as numbers
+// (unlike JsonLogger's "%.3f" strings) for in-process consumers: the daemon's
+// device-counter plugin hands these to the daemon's own sinks.  Not
+// thread-safe; "ts_ms" is the record timestamp in ms since the epoch.
+class RecordLogger : public Logger {
+ public:
+  void setTimestamp(Timestamp ts = std::chrono::system_clock::now()) override { ts_ = ts; }
+  void logInt(const std::string& key, int64_t val) override { rec_[key] = static_cast<long long>(val); }
+  void logFloat(const std::string& key, float val) override { rec_[key] = static_cast<double>(val); }
+  void logUint(const std::string& key, uint64_t val) override { rec_[key] = static_cast<unsigned long long>(val); }
+  void logStr(const std::string& key, const std::string& val) override { rec_[key] = val; }
+  void finalize() override;
+  std::vector<Json> records;
+
+ private:
+  Timestamp ts_{};
+  Json rec_ = Json::object();
+};
+
 // Thread-safe in-memory sink. Each finalize() appends one record
 // {"ts_ms": ..., <keys>...}; bounded by capacity (oldest dropped).
 class MemoryLogger : public JsonLogger {

@@ -503,7 +503,7 @@ TEST(GpuHost, CounterPassesAggregatePerMetric) {
     } else {
       s.derived[DD_FP32_ACTIVE] = 0.25f;
       s.derived[DD_VALU_BUSY_PCT] = 90.0f;
-      s.delta[DP_VALU_FLOPS_FP32] = 2'000'000'000ull;  // 2e9 FLOP in 1 ms = 2 TFLOP/s
+      s.delta[DP_VALU_FLOPS_FP32] = 31'250'000ull;  // x64 lanes = 2e9 FLOP in 1 ms = 2 TFLOP/s
       s.delta[DP_MFMA_MOPS_F32] = 1'000'000ull;         // x512 in 1 ms = 0.512 TFLOP/s
       s.delta[DP_GRBM_COUNT] = 1000;
     }

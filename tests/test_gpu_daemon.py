@@ -92,6 +92,52 @@ def test_out_of_process_device_counters(native_built):
         p.wait()
 
 
+def test_daemon_gpu_counter_selection_and_passes(native_built):
+    """--gpu_counters / --gpu_counter_passes (the reference's --dcgm_fields):
+    the daemon's counter monitor runs the selected passes, reports them in
+    getGpuCounterMonitor, and its records carry the precision pass's DCGM keys
+    (fp16/32/64_active) next to the main pass's MFMA utilisation."""
+    p = subprocess.Popen([sys.executable, "-c", BUSY, "25"], stdout=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().startswith("PID")
+        with DaemonProcess(["--enable_gpu_counters", "--gpu_counter_hz=200",
+                            "--gpu_counter_reporting_interval_s=1",
+                            "--gpu_counter_passes=lean:4,precision:1"]) as d:
+            recs = _wait_records(d, "gpu_counters", lambda r: r.get("counter_samples_precision", 0) > 10)
+            ok = [r for r in recs if r.get("counter_samples_precision", 0) > 10]
+            assert ok, d.log()[-3000:]
+            r = ok[-1]
+            for k in ("fp16_active", "fp32_active", "fp64_active", "valu_busy_pct", "mfma_f32_tflops"):
+                assert k in r, (k, r)
+            assert r["mfma_util"] > 1.0, r  # lean pass, device-wide
+            assert 0 <= r["fp32_active"] <= 1.5, r
+            cfg = d.rpc({"fn": "getGpuCounterMonitor"})
+            assert cfg["status"] == "ok" and cfg["counter_passes"] == "lean:4,precision:1", cfg
+            g0 = cfg["gpus"][0]
+            assert [x["set"] for x in g0["passes"]] == ["lean", "precision"], g0
+            assert "SQ_INSTS_VALU_FLOPS_FP32" in g0["passes"][1]["counters"], g0
+            assert set(g0["passes"][0]["counters"]) == {
+                "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_BF16", "TCC_EA0_RDREQ", "TCC_EA0_WRREQ",
+                "GRBM_GUI_ACTIVE", "GRBM_COUNT"}, g0
+            assert g0["pass_switches"] > 10, g0
+        # a plain set: one pass, exactly those counters
+        with DaemonProcess(["--enable_gpu_counters", "--gpu_counter_hz=100",
+                            "--gpu_counters=GRBM_GUI_ACTIVE,GRBM_COUNT,TCC_EA0_RDREQ"]) as d:
+            deadline = time.time() + 30
+            cfg = {}
+            while time.time() < deadline:
+                cfg = d.rpc({"fn": "getGpuCounterMonitor"})
+                if cfg.get("status") == "ok":
+                    break
+                time.sleep(0.3)
+            g0 = cfg["gpus"][0]
+            assert len(g0["passes"]) == 1
+            assert set(g0["passes"][0]["counters"]) == {"GRBM_GUI_ACTIVE", "GRBM_COUNT", "TCC_EA0_RDREQ"}, g0
+    finally:
+        p.kill()
+        p.wait()
+
+
 def test_gputrace_gpu_kernels(native_built, tmp_path):
     sockdir = tempfile.mkdtemp(prefix="dk", dir="/tmp")
     env = {"KINETO_IPC_SOCKET_DIR": sockdir}
