@@ -94,6 +94,18 @@ bool MetricFrame::addSamples(const std::map<std::string, double>& values, TimePo
   return true;
 }
 
+void MetricFrame::addRow(const std::vector<std::pair<size_t, double>>& values, TimePoint t, double missing) {
+  std::vector<char> seen(byPos_.size(), 0);
+  for (const auto& [pos, v] : values) {
+    if (pos >= byPos_.size() || seen[pos]) continue;
+    seen[pos] = 1;
+    addTo(*byPos_[pos], v);
+  }
+  for (size_t i = 0; i < byPos_.size(); ++i)
+    if (!seen[i]) addTo(*byPos_[i], missing);
+  index_->addSample(t);
+}
+
 bool MetricFrame::addSamples(const std::vector<double>& values, TimePoint t) {
   if (values.size() != order_.size()) return false;
   for (size_t i = 0; i < order_.size(); ++i) addTo(series_.at(order_[i]), values[i]);
