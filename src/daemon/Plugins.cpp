@@ -283,6 +283,25 @@ void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d) {
     j["pids"] = pids;
     return j;
   });
+  // the daemon's device-counter monitor: rate, counter passes, counters
+  disp.add("getGpuCounterMonitor", [](const Json&) -> std::optional<Json> {
+    Json j = Json::object();
+    if (!gGpu.config) {
+      j["status"] = "disabled (start dynolog with --enable_gpu_counters)";
+      return j;
+    }
+    std::string out(1 << 14, '\0');
+    int n = gGpu.config(out.data(), static_cast<int>(out.size()));
+    if (n >= static_cast<int>(out.size())) {
+      out.assign(static_cast<size_t>(n) + 1, '\0');
+      n = gGpu.config(out.data(), static_cast<int>(out.size()));
+    }
+    out.resize(static_cast<size_t>(std::max(n, 0)));
+    std::string e;
+    if (!Json::tryParse(out, &j, &e)) j = Json::object();
+    j["status"] = "ok";
+    return j;
+  });
   disp.addLong("cpuTrace", rpc::asyncCapable(d.jobs(), "cpuTrace",
                                             [](const Json& req) -> std::optional<Json> { return runCpuTrace(req); }));
   disp.add("getTopology", [](const Json&) -> std::optional<Json> {

@@ -25,6 +25,11 @@ struct AmdEventDef {
   const char* desc;
 };
 
+// Zen4 data-fabric DRAM channels per package and the DF event code of
+// channel n's read/write data beats (umask 0x7fe reads, 0x7ff writes).
+constexpr int kZen4DramChannels = 12;
+int zen4DfDramEventCode(int channel);
+
 // Events valid for `arch` (empty for non-AMD or pre-Zen4 archs).
 std::vector<AmdEventDef> amdEventTable(CpuArch arch);
 

@@ -1,6 +1,7 @@
 #include "pmu/Metrics.h"
 
 #include <algorithm>
+#include <cstdio>
 
 #include "pmu/AmdEvents.h"
 
@@ -136,12 +137,33 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
   // --- DRAM bandwidth: Zen5 UMC CAS commands x 64 B, summed over amd_umc_* ---
   std::vector<EventRef> umc = {{"dram_rd_bytes", "amd_umc_*/event=0x0a,rdwrmask=0x1/", 64.0},
                                {"dram_wr_bytes", "amd_umc_*/event=0x0a,rdwrmask=0x2/", 64.0}};
-  add("dram_bandwidth", "DRAM read/write bandwidth from memory-controller CAS commands",
-      {{kZen5, umc}}, [](const auto& c, double s, double, auto& o) {
+  // --- Zen4: data-fabric read/write data beats x 64 B, 12 channels per
+  // package (amd_df, one PMU per package; 24 events split into groups of 4
+  // that the kernel multiplexes).  Reference: AmdEvents.h:58-79 DFPmuMsrAmd,
+  // BuiltinMetrics.cpp:534-570 dram_access_reads (Intel offcore there).
+  auto df = [](bool rd, bool wr, const char* rdNick, const char* wrNick, double scale) {
+    std::vector<EventRef> v;
+    for (int ch = 0; ch < kZen4DramChannels; ++ch) {
+      char spec[64];
+      if (rd) {
+        snprintf(spec, sizeof(spec), "amd_df/event=0x%x,umask=0x7fe/", zen4DfDramEventCode(ch));
+        v.push_back({rdNick, spec, scale});
+      }
+      if (wr) {
+        snprintf(spec, sizeof(spec), "amd_df/event=0x%x,umask=0x7ff/", zen4DfDramEventCode(ch));
+        v.push_back({wrNick, spec, scale});
+      }
+    }
+    return v;
+  };
+  add("dram_bandwidth", "DRAM read/write bandwidth (Zen5: UMC CAS commands; Zen4: DF data beats)",
+      {{kZen5, umc}, {kZen4, df(true, true, "dram_rd_bytes", "dram_wr_bytes", 64.0)}},
+      [](const auto& c, double s, double, auto& o) {
         o["dram_read_gbps"] = ratio(get(c, "dram_rd_bytes"), s) * 1e-9;
         o["dram_write_gbps"] = ratio(get(c, "dram_wr_bytes"), s) * 1e-9;
       },
       true);
+  ms->get("dram_bandwidth")->groupMax = 4;
 
   // --- software events (work everywhere, incl. VMs without a PMU) ---
   add("cpu_clock", "CPU time consumed (ms per second)", {{std::nullopt, {{"cpu_clock", "cpu-clock"}}}},
@@ -184,12 +206,14 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
       },
       true);
   std::vector<EventRef> dramRd = {{"cas_rd", "amd_umc_*/event=0x0a,rdwrmask=0x1/"}};
-  add("dram_access_reads", "DRAM read CAS commands and bytes (all UMCs)", {{kZen5, dramRd}},
+  add("dram_access_reads", "DRAM 64-B reads and bytes (Zen5: all UMCs; Zen4: DF read beats, all channels)",
+      {{kZen5, dramRd}, {kZen4, df(true, false, "cas_rd", "", 1.0)}},
       [](const auto& c, double s, double, auto& o) {
         o["dram_reads_per_s"] = ratio(get(c, "cas_rd"), s);
         o["dram_read_bytes_per_s"] = ratio(get(c, "cas_rd"), s) * 64.0;
       },
       true);
+  ms->get("dram_access_reads")->groupMax = 4;
   std::vector<EventRef> fpi = {{"fp_ops", "cpu:fp_ret_sse_avx_ops.all"},
                                {"sse_instr", "cpu:ex_ret_mmx_fp_instr.sse_instr"},
                                {"instructions", "instructions"}};

@@ -39,6 +39,11 @@ struct MetricDesc {
   std::map<std::optional<CpuArch>, std::vector<EventRef>> eventsByArch;
   DeriveFn derive;
   bool systemWideOnly = false;  // uncore metrics cannot be counted per process
+  // Most events one perf group may hold per PMU instance (0 = no limit).
+  // More events than counters (Zen4 DRAM bandwidth: 24 DF events) are split
+  // into several groups, which the kernel multiplexes (counts scaled by
+  // time_enabled / time_running).
+  size_t groupMax = 0;
 
   // Events for this arch (falls back to the arch-independent entry).
   const std::vector<EventRef>* eventsFor(CpuArch a) const;

@@ -173,6 +173,14 @@ CountReader::CountReader(std::shared_ptr<MetricDesc> metric, const PmuDeviceMana
     }
   }
   const bool perThread = target.pid >= 0 && target.cgroupFd < 0 && target.allThreads;
+  if (metric_->groupMax > 0) {
+    // split each PMU's events into groups of at most groupMax
+    std::map<std::string, std::vector<EventConf>> split;
+    for (auto& [pmuKey, evs] : byPmu)
+      for (size_t i = 0; i < evs.size(); ++i)
+        split[pmuKey + "#" + std::to_string(i / metric_->groupMax)].push_back(evs[i]);
+    byPmu.swap(split);
+  }
   for (auto& [pmuKey, evs] : byPmu) {
     std::vector<std::string> nicks;
     for (const auto& e : evs) nicks.push_back(e.name.substr(0, e.name.find('@')));
