@@ -363,13 +363,17 @@ def take_transposed(x: torch.Tensor):
     """Consumer side: the offered transpose of ``x`` (a 2-D view of the same
     storage, unchanged since), removed from the slot; else None."""
     e = _ACT_T[0]
+    # Every take empties the slot, match or not: the consumer is the first
+    # backward after the offer, so a mismatch (e.g. the logits also fed
+    # another loss and dY is a sum) means the offer is stale.  A kept stale
+    # copy could otherwise match a later dY allocated at the same address.
+    _ACT_T[0] = None
     if e is None or x.dim() != 2:
         return None
     (ptr, ver, shape), xt = e
     if (x.data_ptr() != ptr or x._version != ver or x.numel() != xt.numel()
             or tuple(xt.shape) != (x.shape[1], x.shape[0]) or shape[-1] != x.shape[1]):
         return None
-    _ACT_T[0] = None
     return xt
 
 

@@ -1122,36 +1122,48 @@ Json Agent::kernelCounters(size_t top, std::string* err) const {
   // The dispatch stamps (GPU ticks converted by the runtime) and the sample
   // stamps (host clock after each read returns; the counters were latched at
   // an unknown point inside the ~100-300 us read) do not line up to the
-  // tens of microseconds this needs.  Calibrate: shift the dispatches by
-  // -2..+2 ms in 25 us steps and keep the shift whose fit explains the
-  // samples best (mean R^2 over the metrics); report it.
+  // tens of microseconds this needs.  Calibrate: search the shift of the
+  // dispatches in -2..+2 ms that explains the samples best (mean R^2 over the
+  // metrics), coarse to fine -- 250 us steps, then 25 us steps around the
+  // best -- with fits capped at 200 sweeps during the search, and one full
+  // fit at the chosen shift (38 capped fits instead of 161 full ones: the
+  // control thread answers the trace request promptly).
   const uint32_t nCls = static_cast<uint32_t>(kernelOf.size());
-  auto fitAt = [&](int64_t shiftNs) {
+  auto fitAt = [&](int64_t shiftNs, int sweeps) {
     std::vector<KcSpan> sh(spans);
     for (auto& sp : sh) {
       sp.start = static_cast<uint64_t>(static_cast<int64_t>(sp.start) + shiftNs);
       sp.end = static_cast<uint64_t>(static_cast<int64_t>(sp.end) + shiftNs);
     }
-    return attributeCounters(sh, nCls, samples);
+    return attributeCounters(sh, nCls, samples, 2e6, sweeps);
   };
   auto score = [](const KcResult& r) {  // busy share barely varies: not scored
     double s = 0;
     for (int m = KC_MFMA; m < KC_NUM; ++m) s += r.r2[m];
     return s / (KC_NUM - KC_MFMA);
   };
+  constexpr int kSearchSweeps = 200;
   int64_t bestShift = 0;
-  KcResult res = fitAt(0);
-  double best = score(res);
-  for (int64_t sh = -2000000; sh <= 2000000; sh += 25000) {
+  double best = score(fitAt(0, kSearchSweeps));
+  for (int64_t sh = -2000000; sh <= 2000000; sh += 250000) {
     if (sh == 0) continue;
-    KcResult r = fitAt(sh);
-    const double sc = score(r);
+    const double sc = score(fitAt(sh, kSearchSweeps));
     if (sc > best) {
       best = sc;
       bestShift = sh;
-      res = std::move(r);
     }
   }
+  const int64_t center = bestShift;
+  for (int64_t sh = center - 225000; sh <= center + 225000; sh += 25000) {
+    if (sh == center || sh < -2000000 || sh > 2000000) continue;
+    const double sc = score(fitAt(sh, kSearchSweeps));
+    if (sc > best) {
+      best = sc;
+      bestShift = sh;
+    }
+  }
+  KcResult res = fitAt(bestShift, 2000);
+  best = score(res);
   std::vector<uint32_t> order(kernelOf.size());
   for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
   std::sort(order.begin(), order.end(),

@@ -13,7 +13,7 @@ const char* kcMetricName(int m) {
 }
 
 KcResult attributeCounters(const std::vector<KcSpan>& spansIn, uint32_t nClasses,
-                           const std::vector<KcSample>& samplesIn, double minCoverNs) {
+                           const std::vector<KcSample>& samplesIn, double minCoverNs, int maxSweeps) {
   KcResult res;
   res.classes.resize(nClasses);
   for (uint32_t c = 0; c < nClasses; ++c) res.classes[c].cls = c;
@@ -88,7 +88,7 @@ KcResult attributeCounters(const std::vector<KcSpan>& spansIn, uint32_t nClasses
     if (var[c] >= 0)
       for (int m = 0; m < KC_NUM; ++m) x[static_cast<size_t>(var[c]) * KC_NUM + m] = res.classes[c].mixed[m];
   for (int m = 0; m < KC_NUM; ++m) {
-    for (int sweep = 0; sweep < 2000; ++sweep) {
+    for (int sweep = 0; sweep < maxSweeps; ++sweep) {
       double moved = 0, scale = 0;
       for (int k = 0; k < K; ++k) {
         const double gkk = G[static_cast<size_t>(k) * K + k];

@@ -67,12 +67,14 @@ def test_weight_transpose_registry_invalidation():
 
 def test_activation_transpose_slot_offer_take():
     """ops.offer_transposed / take_transposed: one slot, served once to a 2-D
-    view of the same storage, refused after a write or for another tensor,
-    replaced by the next offer."""
+    view of the same storage, refused after a write or for another tensor
+    (and then dropped: every take empties the slot), replaced by the next offer."""
     x = torch.randn(8, 6)
     xt = x.t().contiguous()
     ops.offer_transposed(x, xt)
-    assert ops.take_transposed(torch.randn(8, 6)) is None  # another tensor
+    assert ops.take_transposed(torch.randn(8, 6)) is None  # another tensor: the offer is stale
+    assert ops._ACT_T[0] is None  # ... and dropped, never served later
+    ops.offer_transposed(x, xt)
     assert ops.take_transposed(x.view(2, 4, 6).reshape(-1, 6)) is xt  # a view of it: served
     assert ops.take_transposed(x) is None  # served once
     ops.offer_transposed(x, xt)

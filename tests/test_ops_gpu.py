@@ -275,6 +275,39 @@ def test_fused_adamw_per_param_step_counts(ops):
         assert diff <= 2e-2, diff
 
 
+def test_fused_adamw_loads_torch_adamw_state(ops):
+    """A torch.optim.AdamW state dict (step counts stored as 0-d tensors) loads
+    into FusedAdamW and the next steps keep tracking torch's trajectory."""
+    from dynolog_amd.ops.optim import FusedAdamW
+
+    g = torch.Generator(device=DEV).manual_seed(21)
+    base = [torch.randn(s, device=DEV, generator=g).bfloat16() for s in [(512, 256), (777,)]]
+    pa = [torch.nn.Parameter(b.clone()) for b in base]
+    pb = [torch.nn.Parameter(b.clone()) for b in base]
+    hp = dict(lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    ob = torch.optim.AdamW(pb, fused=True, **hp)
+    for _ in range(3):
+        for a, b in zip(pa, pb):
+            gr = torch.randn(a.shape, device=DEV, generator=g).bfloat16()
+            b.grad = gr
+        ob.step()
+    for a, b in zip(pa, pb):
+        a.data.copy_(b.data)
+    oa = FusedAdamW(pa, **hp)
+    oa.load_state_dict(ob.state_dict())
+    assert torch.is_tensor(oa.state[pa[0]]["step"])  # as torch stores it
+    for _ in range(2):
+        for a, b in zip(pa, pb):
+            gr = torch.randn(a.shape, device=DEV, generator=g).bfloat16()
+            a.grad, b.grad = gr.clone(), gr.clone()
+        oa.step()
+        ob.step()
+    assert oa.state[pa[0]]["step"] == 5 and isinstance(oa.state[pa[0]]["step"], int)
+    for a, b in zip(pa, pb):
+        diff = (a.float() - b.float()).abs().max().item()
+        assert diff <= 2e-2, diff
+
+
 def test_fused_adamw_transposed_copies(ops):
     """FusedAdamW(transposed=...) updates 2-D weights exactly like the flat
     kernel (bitwise p, m, v) and writes W^T bitwise; ops.dgrad then uses the
