@@ -18,12 +18,20 @@ const char* cpuArchName(CpuArch a) {
     case CpuArch::AmdZen4: return "zen4";
     case CpuArch::AmdZen5: return "zen5";
     case CpuArch::IntelGeneric: return "intel";
+    case CpuArch::IntelSkylakeX: return "intel_skx";
+    case CpuArch::IntelIceLakeX: return "intel_icx";
+    case CpuArch::IntelSapphireRapids: return "intel_spr";
     default: return "unknown";
   }
 }
 
 CpuArch makeCpuArch(CpuVendor v, int family, int model) {
-  if (v == CpuVendor::Intel) return CpuArch::IntelGeneric;
+  if (v == CpuVendor::Intel) {
+    if (family == 6 && model == 0x55) return CpuArch::IntelSkylakeX;
+    if (family == 6 && (model == 0x6a || model == 0x6c)) return CpuArch::IntelIceLakeX;
+    if (family == 6 && (model == 0x8f || model == 0xcf)) return CpuArch::IntelSapphireRapids;
+    return CpuArch::IntelGeneric;
+  }
   if (v != CpuVendor::Amd) return CpuArch::Unknown;
   if (family == 0x17) return model >= 0x30 ? CpuArch::AmdZen2 : CpuArch::AmdZen1;
   if (family == 0x19) {

@@ -31,6 +31,9 @@ enum class CpuArch {
   Unknown,
   AmdZen1, AmdZen2, AmdZen3, AmdZen4, AmdZen5,
   IntelGeneric,
+  IntelSkylakeX,        // family 6 model 0x55: Skylake-SP / Cascade Lake / Cooper Lake
+  IntelIceLakeX,        // 0x6a, 0x6c: Ice Lake-SP / -D
+  IntelSapphireRapids,  // 0x8f, 0xcf: Sapphire / Emerald Rapids
 };
 const char* cpuArchName(CpuArch a);
 CpuArch makeCpuArch(CpuVendor v, int family, int model);
