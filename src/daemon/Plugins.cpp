@@ -3,6 +3,7 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <memory>
@@ -85,6 +86,7 @@ struct GpuPlugin {
   int (*config)(char*, int) = nullptr;
 };
 GpuPlugin gGpu;
+std::atomic<bool> gGpuStarted{false};  // the monitor finished start(): config() is safe
 
 std::string exeDir() {
   char buf[PATH_MAX];
@@ -232,6 +234,7 @@ void startGpuCounterMonitor(Daemon& d) {
                << (gGpu.lastError ? gGpu.lastError() : "?");
     return;
   }
+  gGpuStarted = true;
   d.addLoop("gpucounters", FLAGS_gpu_counter_reporting_interval_s * 1000, [&d] {
     Json recs;
     std::string e;
@@ -309,7 +312,7 @@ void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d) {
   // the daemon's device-counter monitor: rate, counter passes, counters
   disp.add("getGpuCounterMonitor", [](const Json&) -> std::optional<Json> {
     Json j = Json::object();
-    if (!gGpu.config) {
+    if (!gGpu.config || !gGpuStarted.load()) {
       j["status"] = "disabled (start dynolog with --enable_gpu_counters)";
       return j;
     }
@@ -342,6 +345,7 @@ void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d) {
 }
 
 void stopPlugins() {
+  gGpuStarted = false;
   if (gGpu.handle && gGpu.stop) gGpu.stop();
   {
     std::lock_guard<std::mutex> g(gPerfMu);
