@@ -61,6 +61,9 @@ def parse_args(argv=None):
     p.add_argument("--pack-batch", type=int, default=32)
     p.add_argument("--gather-mode", default="gather", choices=["gather", "allgather", "shm", "none"])
     p.add_argument("--counter-set", default="lite", help="lite (default) | full | lean | core | comma list")
+    p.add_argument("--counter-passes", default="",
+                   help="rotate counter configs per pack batch, e.g. lite:3,precision:1 "
+                        "(adds fp16/32/64_active); empty = one pass of --counter-set")
     p.add_argument("--no-agent", action="store_true", help="run the workload only")
     p.add_argument("--optimizer", default="fused", choices=["fused", "torch"],
                    help="fused: one-launch CDNA4 AdamW (dynolog_amd.ops.optim); torch: AdamW(fused=True)")
@@ -198,7 +201,7 @@ def main(argv=None) -> int:
         ag = dagent.GpuAgent.start(device=pdist.device_index(env), rank=env.rank, world=env.world,
                                    sample_hz=args.sample_hz, batch=args.pack_batch,
                                    gather_mode=args.gather_mode, log_file=args.log_file,
-                                   counter_set=args.counter_set,
+                                   counter_set=args.counter_set, counter_passes=args.counter_passes,
                                    sinks=("json", "memory"))
 
     # Host CPU PMU co-sampler (one daemon per node, on local rank 0), counting
@@ -372,6 +375,7 @@ def main(argv=None) -> int:
                 "model": args.model, "global_batch": B * env.world, "seq_len": S,
                 "parallelism": f"dp{env.world}", "sample_hz_target": args.sample_hz,
                 "counter_set": args.counter_set,
+                "counter_passes": args.counter_passes or None,
                 "gather": ag.config.get("gather_mode", args.gather_mode) if ag else args.gather_mode,
                 "pack_batch": args.pack_batch,
                 "kernel_trace_ready": args.kernel_trace_ready, "phases": args.phases,
