@@ -120,7 +120,7 @@ def run_baseline_child(args, tag: str) -> dict:
     t0 = time.time()
     try:
         # the child's stdout goes to stderr: rank 0's stdout carries ONE result line
-        r = subprocess.run(cmd, env=env, stdout=sys.stderr, timeout=1800)
+        r = subprocess.run(cmd, env=env, stdout=sys.stderr, timeout=600)
         res = {"tag": tag, "rc": r.returncode, "wall_s": round(time.time() - t0, 1)}
         if r.returncode == 0 and os.path.getsize(path) > 0:
             with open(path) as f:
@@ -419,7 +419,11 @@ def main(argv=None) -> int:
             out["agent"] = {k: agent_stats.get(k) for k in
                             ("samples_taken", "samples_failed", "sample_latency_us_avg",
                              "sample_latency_us_max", "late_ticks", "stage_waits", "stage_wait_ms",
-                             "gathers", "raw_instances", "last_error")}
+                             "gathers", "raw_instances", "last_error", "gather_latency_us_avg",
+                             "gather_latency_us_max", "gather_latency_samples", "gather_bytes",
+                             "gather_slots", "gather_cap_slots_now", "gather_backlog", "drain_bytes",
+                             "counter_passes", "pass_switches", "pass_switch_us_avg")
+                            if k in agent_stats}
         if args.host_pmu != "off":
             # one co-sampler per node (local rank 0): every node's summary
             # reaches the result line, keyed by host when there are several

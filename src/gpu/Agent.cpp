@@ -298,6 +298,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   sizer_.reset(cfg_.gatherCapSlots, GatherSizer::kQuantum, GatherSizer::kDefaultLag);
   static_assert(kAgree > GatherSizer::kDefaultLag, "agreement entries must outlive the lag");
   gatherBytes_ = gatherSlots_ = drainBytes_ = runAheadWaits_ = 0;
+  gatherTimed_ = gatherLatSumNs_ = gatherLatMaxNs_ = gatherLatLastNs_ = 0;
   backlogNow_ = 0;
   capNow_ = cfg_.gatherCapSlots;
   gatherFailed_ = false;
@@ -698,7 +699,49 @@ bool Agent::step(hipStream_t stream, std::string* err) {
   // stream never waits on the (lowest-priority) pack stream.  A pack still
   // queued behind the step's own kernels is picked up by the next step.
   const uint64_t head = completedPackHead();
-  if (collective_) return gatherCollective(stream, head, err);
+  harvestGatherTimers();
+  const int timer = beginGatherTimer(stream);
+  const bool ok = collective_ ? gatherCollective(stream, head, err) : gatherLocal(stream, head, err);
+  if (timer >= 0) endGatherTimer(timer, stream);
+  return ok;
+}
+
+int Agent::beginGatherTimer(hipStream_t stream) {
+  const int i = gatherTimerNext_;
+  GatherTimer& t = gatherTimers_[i];
+  if (t.pending) return -1;  // its gather has not finished yet: skip timing this one
+  if (!t.t0 && (hipEventCreate(&t.t0) != hipSuccess || hipEventCreate(&t.t1) != hipSuccess)) return -1;
+  if (hipEventRecord(t.t0, stream) != hipSuccess) return -1;
+  return i;
+}
+
+void Agent::endGatherTimer(int idx, hipStream_t stream) {
+  GatherTimer& t = gatherTimers_[idx];
+  if (hipEventRecord(t.t1, stream) != hipSuccess) return;
+  t.pending = true;
+  gatherTimerNext_ = (idx + 1) % kGatherTimers;
+}
+
+void Agent::harvestGatherTimers() {
+  for (auto& t : gatherTimers_) {
+    if (!t.pending || hipEventQuery(t.t1) != hipSuccess) continue;
+    float ms = 0.f;
+    t.pending = false;
+    if (hipEventElapsedTime(&ms, t.t0, t.t1) != hipSuccess || ms < 0.f) continue;
+    const uint64_t ns = static_cast<uint64_t>(ms * 1e6);
+    gatherTimed_++;
+    gatherLatSumNs_ += ns;
+    gatherLatLastNs_ = ns;
+    uint64_t mx = gatherLatMaxNs_.load();
+    while (ns > mx && !gatherLatMaxNs_.compare_exchange_weak(mx, ns)) {
+    }
+  }
+}
+
+// world 1, or the shm mailbox: gather_prep straight into a drain buffer (or
+// into this rank's mailbox block)
+bool Agent::gatherLocal(hipStream_t stream, uint64_t head, std::string* err) {
+  (void)err;
   const auto rg = planGatherRange(head, gatheredHost_, cfg_.gatherCapSlots, cfg_.ringSlots);
   if (shmMode_ && cfg_.rank != 0) {
     uint8_t* blk = shm_->reserve(cfg_.rank, shmEnq_);
@@ -1279,6 +1322,16 @@ void Agent::releaseDevice() {
   freeDev(dAgree_);
   freeHost(hAgree_);
   for (auto& e : agreeDone_) destroyEvent(e);
+  {
+    std::lock_guard<std::mutex> g(stepMu_);
+    harvestGatherTimers();
+    for (auto& t : gatherTimers_) {
+      destroyEvent(t.t0);
+      destroyEvent(t.t1);
+      t.pending = false;
+    }
+    gatherTimerNext_ = 0;
+  }
   if (packStream_) hipWarn(hipStreamDestroy(packStream_), "hipStreamDestroy pack");
   if (drainStream_) hipWarn(hipStreamDestroy(drainStream_), "hipStreamDestroy drain");
   packStream_ = drainStream_ = nullptr;
@@ -1312,6 +1365,12 @@ Json Agent::stats() const {
   j["gather_cap_slots_now"] = static_cast<unsigned long long>(capNow_.load());
   j["gather_backlog"] = static_cast<unsigned long long>(backlogNow_.load());
   j["gather_run_ahead_waits"] = static_cast<unsigned long long>(runAheadWaits_.load());
+  // trainer-stream time of a gather (gather_prep + size all-reduce + collective)
+  const uint64_t nt = gatherTimed_.load();
+  j["gather_latency_samples"] = static_cast<unsigned long long>(nt);
+  j["gather_latency_us_avg"] = nt ? gatherLatSumNs_.load() / static_cast<double>(nt) * 1e-3 : 0.0;
+  j["gather_latency_us_max"] = gatherLatMaxNs_.load() * 1e-3;
+  j["gather_latency_us_last"] = gatherLatLastNs_.load() * 1e-3;
   if (cfg_.rank == 0) j["drain_bytes"] = static_cast<unsigned long long>(drainBytes_.load());
   if (shmMode_) j["shm_full_steps"] = static_cast<unsigned long long>(shmFull_.load());
   if (slotRing_) {

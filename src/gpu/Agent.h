@@ -226,6 +226,22 @@ class Agent {
   std::atomic<uint64_t> gatherBytes_{0}, gatherSlots_{0}, drainBytes_{0}, runAheadWaits_{0};
   std::atomic<uint64_t> backlogNow_{0}, capNow_{0};
   bool gatherCollective(hipStream_t stream, uint64_t head, std::string* err);
+  bool gatherLocal(hipStream_t stream, uint64_t head, std::string* err);
+
+  // Gather latency on the trainer's stream (gather_prep through the end of the
+  // collective / drain hand-off): timing events around each gather, harvested
+  // by a later step once complete (host query; never waited on).
+  struct GatherTimer {
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    bool pending = false;
+  };
+  static constexpr int kGatherTimers = 16;
+  GatherTimer gatherTimers_[kGatherTimers];
+  int gatherTimerNext_ = 0;
+  int beginGatherTimer(hipStream_t stream);  // -1: no free timer (stepMu_)
+  void endGatherTimer(int idx, hipStream_t stream);
+  void harvestGatherTimers();
+  std::atomic<uint64_t> gatherTimed_{0}, gatherLatSumNs_{0}, gatherLatMaxNs_{0}, gatherLatLastNs_{0};
 
   ncclComm_t comm_ = nullptr;
   // gather_mode "shm" (world > 1, one node): ranks > 0 publish their payload

@@ -343,6 +343,9 @@ def test_rccl_gather_path_with_one_rank(native_built, mode):
     full = 64 + 4096 * 256
     assert st["gather_bytes"] < 4 * full + (st["gathers"] - 4) * 0.1 * full, st
     assert st["gather_cap_slots_now"] < 4096, st
+    # trainer-stream gather latency, harvested from completed timing events
+    assert st["gather_latency_samples"] >= 30, st
+    assert 0 < st["gather_latency_us_avg"] <= st["gather_latency_us_max"] < 100000, st
 
 
 def test_agent_restart_returns_device_memory(native_built):
