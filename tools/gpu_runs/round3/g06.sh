@@ -1,11 +1,13 @@
 # round 3 g06: full GPU suite on the current tree (counter selection, AdamW state
 # load, coarse-to-fine kernel counters), smoke, sampler-kernel stats (main +
 # precision pack, gather_prep, drain compaction) and the headline bench with the
-# rotating precision pass
+# rotating precision pass; the counter probe again with its fp16 burn fixed (a constant
+# guard fp16 cannot represent had let the compiler drop the loop)
 set -o pipefail
 O=gpurun_out/g06; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o pack -- python3 tools/bench_pack_kernel.py --iters 100 > $O/prof.log 2>&1 && \
-timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --counter-passes lite:3,precision:1 --no-agent-baseline off --json-out $O/bench_passes.json > $O/bench_passes.log 2>&1
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --counter-passes lite:3,precision:1 --no-agent-baseline off --json-out $O/bench_passes.json > $O/bench_passes.log 2>&1 && \
+timeout -k 10 120 ./build/probes/probe_passes $O/counters.txt > $O/probe_passes.log 2>&1

@@ -72,7 +72,8 @@ __global__ __launch_bounds__(256) void k_fp16(float* out, int iters, float scale
     a = a * b + c;
     c = c * b + a;
   }
-  if ((float)(a[0] + c[1]) == 1234.5f) out[threadIdx.x] = (float)a[0];
+  // run-time sentinel: fp16 cannot hold 1234.5, so a constant guard let the compiler drop the loop
+  if ((float)(a[0] + c[1]) == -scale * 1234.5f) out[threadIdx.x] = (float)a[0];
 }
 __global__ __launch_bounds__(256) void k_mfma(float* out, int iters) {
   bf16x8 a, b;
