@@ -37,6 +37,15 @@ const AmdEventDef kZenCore[] = {
     {"cpu", "ls_l1_d_tlb_miss.all", "event=0x45,umask=0xff", "L1 DTLB misses (all page sizes)"},
     {"cpu", "ls_dmnd_fills_from_sys.all", "event=0x43,umask=0xff", "Demand data cache fills by source"},
     {"cpu", "ls_any_fills_from_sys.all", "event=0x44,umask=0xff", "Any data cache fills by source"},
+    {"cpu", "ls_any_fills_from_sys.local_l2", "event=0x44,umask=0x01", "Data cache fills from the local L2"},
+    {"cpu", "ls_any_fills_from_sys.local_ccx", "event=0x44,umask=0x02", "Data cache fills from the local L3 / CCX"},
+    {"cpu", "ls_any_fills_from_sys.remote_cache", "event=0x44,umask=0x14",
+     "Data cache fills from another CCX's cache (this or the other socket)"},
+    {"cpu", "ls_any_fills_from_sys.dram_io_all", "event=0x44,umask=0x48", "Data cache fills from DRAM or IO"},
+    {"cpu", "ls_alloc_mab_count", "event=0x5f", "Miss address buffers in use per cycle (L1D misses in flight)"},
+    {"cpu", "ex_no_retire.not_complete", "event=0xd6,umask=0x02", "Cycles the oldest op was not complete"},
+    {"cpu", "ex_no_retire.load_not_complete", "event=0xd6,umask=0xa2",
+     "Cycles the oldest op was a load that was not complete"},
     {"cpu", "l2_request_g1.all", "event=0x60,umask=0xff", "L2 requests (group 1)"},
     {"cpu", "l2_cache_req_stat.ic_dc_miss_in_l2", "event=0x64,umask=0x09", "IC+DC demand requests missing L2"},
     {"cpu", "l2_cache_req_stat.ic_dc_hit_in_l2", "event=0x64,umask=0xf6", "IC+DC demand requests hitting L2"},

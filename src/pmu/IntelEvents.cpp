@@ -42,6 +42,28 @@ const AmdEventDef kSkx[] = {
     {"cpu", "int_misc.recovery_cycles", "event=0x0d,umask=0x01", "Cycles the allocator stalls for recovery"},
 };
 
+// Skylake-SP and Ice Lake-SP stall-cycle events (CYCLE_ACTIVITY: the counter
+// mask selects cycles with at least one outstanding miss of that level while
+// execution stalled) for the reference's topdown_l3_L1_bound / L2_bound ids.
+const AmdEventDef kSkxIcxStalls[] = {
+    {"cpu", "cycle_activity.stalls_mem_any", "event=0xa3,umask=0x14,cmask=0x14",
+     "Execution stalls while a memory load is outstanding"},
+    {"cpu", "cycle_activity.stalls_l1d_miss", "event=0xa3,umask=0x0c,cmask=0x0c",
+     "Execution stalls while an L1D miss is outstanding"},
+    {"cpu", "cycle_activity.stalls_l2_miss", "event=0xa3,umask=0x05,cmask=0x05",
+     "Execution stalls while an L2 miss is outstanding"},
+    {"cpu", "icache_16b.ifdata_stall", "event=0x80,umask=0x04", "Cycles fetch stalled on an instruction cache miss"},
+};
+
+// Skylake-SP off-core data reads (topdown_l4_mem: DRAM latency by Little's law)
+const AmdEventDef kSkxOffcore[] = {
+    {"cpu", "offcore_requests_outstanding.all_data_rd", "event=0x60,umask=0x08",
+     "Off-core data reads outstanding, per cycle"},
+    {"cpu", "offcore_requests_outstanding.cycles_with_data_rd", "event=0x60,umask=0x08,cmask=0x01",
+     "Cycles with at least one off-core data read outstanding"},
+    {"cpu", "offcore_requests.all_data_rd", "event=0xb0,umask=0x08", "Off-core data read requests"},
+};
+
 // Ice Lake-SP and Sapphire Rapids page walks.
 const AmdEventDef kIcxSpr[] = {
     {"cpu", "dtlb_load_misses.walk_completed", "event=0x12,umask=0x0e", "Completed page walks of load DTLB misses"},
@@ -61,8 +83,14 @@ std::vector<AmdEventDef> intelEventTable(CpuArch arch) {
   v.insert(v.end(), std::begin(kArch), std::end(kArch));
   if (arch == CpuArch::IntelGeneric) return v;
   v.insert(v.end(), std::begin(kFp), std::end(kFp));
-  if (arch == CpuArch::IntelSkylakeX) v.insert(v.end(), std::begin(kSkx), std::end(kSkx));
-  else v.insert(v.end(), std::begin(kIcxSpr), std::end(kIcxSpr));
+  if (arch == CpuArch::IntelSkylakeX) {
+    v.insert(v.end(), std::begin(kSkx), std::end(kSkx));
+    v.insert(v.end(), std::begin(kSkxOffcore), std::end(kSkxOffcore));
+  } else {
+    v.insert(v.end(), std::begin(kIcxSpr), std::end(kIcxSpr));
+  }
+  if (arch != CpuArch::IntelSapphireRapids) v.insert(v.end(), std::begin(kSkxIcxStalls), std::end(kSkxIcxStalls));
+  else v.push_back({"cpu", "icache_data.stalls", "event=0x80,umask=0x04", "Cycles fetch stalled on an instruction cache miss"});
   return v;
 }
 

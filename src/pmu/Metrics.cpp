@@ -304,6 +304,137 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
         o["return_mpki"] = ratio(get(c, "ret_misp"), get(c, "instructions")) * 1e3;
         o["branch_miss_rate"] = ratio(get(c, "brn_misp"), get(c, "brn"));
       });
+
+  // --- the rest of the reference's ids (BuiltinMetrics.cpp:762-1048) ---
+  // dqos: IPC next to the scheduler's view of the host.  The sched_stat_*
+  // tracepoints carry __perf_count(delay / runtime), so counting them sums
+  // nanoseconds; they need root and kernel.sched_schedstats=1 (the metric
+  // opens what it can: without them the IPC / fault / switch rates remain).
+  add("dqos", "Host QoS estimate: IPC, switches, faults and scheduler run / wait / sleep / block time",
+      {{std::nullopt,
+        {{"cpu_clock", "cpu-clock"}, {"instructions", "instructions"}, {"cycles", "cycles"},
+         {"cs", "context-switches"}, {"pf_min", "minor-faults"}, {"pf_maj", "major-faults"},
+         {"align", "alignment-faults"}, {"runtime_ns", "tracepoint:sched:sched_stat_runtime"},
+         {"wait_ns", "tracepoint:sched:sched_stat_wait"}, {"sleep_ns", "tracepoint:sched:sched_stat_sleep"},
+         {"iowait_ns", "tracepoint:sched:sched_stat_iowait"}, {"blocked_ns", "tracepoint:sched:sched_stat_blocked"}}}},
+      [](const auto& c, double s, double, auto& o) {
+        o["ipc"] = ratio(get(c, "instructions"), get(c, "cycles"));
+        o["cpu_clock_ms_per_s"] = ratio(get(c, "cpu_clock"), s) * 1e-6;
+        o["context_switches_per_s"] = ratio(get(c, "cs"), s);
+        o["minor_faults_per_s"] = ratio(get(c, "pf_min"), s);
+        o["major_faults_per_s"] = ratio(get(c, "pf_maj"), s);
+        o["alignment_faults_per_s"] = ratio(get(c, "align"), s);
+        for (const char* k : {"runtime_ns", "wait_ns", "sleep_ns", "iowait_ns", "blocked_ns"}) {
+          if (!c.count(k)) continue;
+          std::string key = std::string("sched_") + k;
+          key.replace(key.size() - 3, 3, "_ms_per_s");
+          o[key] = ratio(get(c, k), s) * 1e-6;
+        }
+        // share of runnable time spent waiting for a CPU: the QoS signal
+        if (c.count("runtime_ns") && c.count("wait_ns"))
+          o["sched_wait_ratio"] = ratio(get(c, "wait_ns"), get(c, "runtime_ns") + get(c, "wait_ns"));
+      });
+  // cs_ipc: IPC and work per context switch (the reference samples it every
+  // switch; counted here, the same ratios over the interval)
+  add("cs_ipc", "IPC and instructions / cycles per context switch",
+      {{std::nullopt, {{"cs", "context-switches"}, {"cycles", "cycles"}, {"instructions", "instructions"}}}},
+      [](const auto& c, double, double, auto& o) {
+        o["cs_ipc"] = ratio(get(c, "instructions"), get(c, "cycles"));
+        o["instructions_per_cs"] = ratio(get(c, "instructions"), get(c, "cs"));
+        o["cycles_per_cs"] = ratio(get(c, "cycles"), get(c, "cs"));
+      });
+  // topdown_l4_mem: memory-level parallelism and load-miss latency by
+  // Little's law (in-flight misses per cycle / misses).  Zen: L1D miss
+  // address buffers and fills by source; Skylake-SP: off-core data reads.
+  std::vector<EventRef> memZen = {{"cycles", "cpu:ls_not_halted_cyc"},
+                                  {"outstanding", "cpu:ls_alloc_mab_count"},
+                                  {"requests", "cpu:ls_any_fills_from_sys.all"},
+                                  {"dram_fills", "cpu:ls_any_fills_from_sys.dram_io_all"}};
+  std::vector<EventRef> memSkx = {{"cycles", "cycles"},
+                                  {"outstanding", "cpu:offcore_requests_outstanding.all_data_rd"},
+                                  {"active", "cpu:offcore_requests_outstanding.cycles_with_data_rd"},
+                                  {"requests", "cpu:offcore_requests.all_data_rd"}};
+  add("topdown_l4_mem", "Memory-level parallelism and miss latency (Zen: L1D misses; Skylake-SP: off-core reads)",
+      {{kZen4, memZen}, {kZen5, memZen}, {kSkx, memSkx}}, [](const auto& c, double s, double, auto& o) {
+        o["mem_outstanding_avg"] = ratio(get(c, "outstanding"), get(c, "cycles"));
+        o["mem_latency_cycles"] = ratio(get(c, "outstanding"), get(c, "requests"));
+        if (c.count("active")) o["mem_active_pct"] = ratio(get(c, "active"), get(c, "cycles")) * 100.0;
+        if (c.count("dram_fills")) {
+          o["dram_fills_per_s"] = ratio(get(c, "dram_fills"), s);
+          o["dram_fill_pct"] = ratio(get(c, "dram_fills"), get(c, "requests")) * 100.0;
+        }
+      });
+  // topdown_l3_icache: Intel counts fetch stalls on an I-cache miss; Zen has
+  // no such event, so it reports front-end latency cycles (no op delivered
+  // to any dispatch slot: I-cache / ITLB misses and redirects) and the
+  // I-cache miss rate
+  auto feLat = [](CpuArch a) {
+    char spec[64];
+    snprintf(spec, sizeof(spec), "cpu/event=0x1a0,umask=0x1,cmask=0x%x/", amdDispatchSlots(a));
+    return std::vector<EventRef>{{"cycles", "cpu:ls_not_halted_cyc"}, {"fe_latency", spec},
+                                 {"instructions", "instructions"},
+                                 {"ic_miss", "cpu:ic_tag_hit_miss.instruction_cache_miss"}};
+  };
+  std::vector<EventRef> icSkx = {{"cycles", "cycles"}, {"ic_stall", "cpu:icache_16b.ifdata_stall"}};
+  std::vector<EventRef> icSpr = {{"cycles", "cycles"}, {"ic_stall", "cpu:icache_data.stalls"}};
+  add("topdown_l3_icache", "Instruction-fetch stalls (Intel: I-cache miss stall cycles; Zen: front-end latency cycles)",
+      {{kZen4, feLat(kZen4)}, {kZen5, feLat(kZen5)}, {kSkx, icSkx}, {kIcx, icSkx}, {kSpr, icSpr}},
+      [](const auto& c, double, double, auto& o) {
+        if (c.count("ic_stall")) o["icache_stall_pct"] = ratio(get(c, "ic_stall"), get(c, "cycles")) * 100.0;
+        if (c.count("fe_latency")) o["frontend_latency_pct"] = ratio(get(c, "fe_latency"), get(c, "cycles")) * 100.0;
+        if (c.count("ic_miss")) o["icache_mpki"] = ratio(get(c, "ic_miss"), get(c, "instructions")) * 1e3;
+      });
+  // topdown_l3_L1_bound: Intel stall cycles with a load outstanding but no
+  // L1D miss.  Zen has no per-level stall counters; its level-2 split of the
+  // back end (stalled slots x share of incomplete-load cycles) stands in
+  auto memBound = [](CpuArch a) {
+    return std::vector<EventRef>{{"slots", "cpu:ls_not_halted_cyc", static_cast<double>(amdDispatchSlots(a))},
+                                 {"be_stall", "cpu:de_no_dispatch_per_slot.backend_stalls"},
+                                 {"load_nc", "cpu:ex_no_retire.load_not_complete"},
+                                 {"not_complete", "cpu:ex_no_retire.not_complete"}};
+  };
+  std::vector<EventRef> l1b = {{"cycles", "cycles"},
+                               {"stalls_mem", "cpu:cycle_activity.stalls_mem_any"},
+                               {"stalls_l1d", "cpu:cycle_activity.stalls_l1d_miss"}};
+  add("topdown_l3_L1_bound", "Stalls on loads that hit L1D (Intel); memory- vs core-bound back end (Zen)",
+      {{kZen4, memBound(kZen4)}, {kZen5, memBound(kZen5)}, {kSkx, l1b}, {kIcx, l1b}},
+      [](const auto& c, double, double, auto& o) {
+        if (c.count("stalls_mem")) {
+          const double cyc = get(c, "cycles");
+          o["topdown_memory_bound_pct"] = ratio(get(c, "stalls_mem"), cyc) * 100.0;
+          o["topdown_l1_bound_pct"] = ratio(std::max(0.0, get(c, "stalls_mem") - get(c, "stalls_l1d")), cyc) * 100.0;
+          return;
+        }
+        const double be = ratio(get(c, "be_stall"), get(c, "slots"));
+        const double memShare = std::min(1.0, ratio(get(c, "load_nc"), get(c, "not_complete")));
+        o["topdown_backend_bound_pct"] = be * 100.0;
+        o["topdown_memory_bound_pct"] = be * memShare * 100.0;
+        o["topdown_core_bound_pct"] = be * (1.0 - memShare) * 100.0;
+      });
+  // topdown_l3_L2_bound: Intel stall cycles with an L1D miss outstanding
+  // that hit L2.  Zen: where L1D fills come from (local L2, local L3, other
+  // CCX caches, DRAM / IO)
+  std::vector<EventRef> fillsZen = {{"fills", "cpu:ls_any_fills_from_sys.all"},
+                                    {"fill_l2", "cpu:ls_any_fills_from_sys.local_l2"},
+                                    {"fill_l3", "cpu:ls_any_fills_from_sys.local_ccx"},
+                                    {"fill_remote", "cpu:ls_any_fills_from_sys.remote_cache"},
+                                    {"fill_dram", "cpu:ls_any_fills_from_sys.dram_io_all"}};
+  std::vector<EventRef> l2b = {{"cycles", "cycles"},
+                               {"stalls_l1d", "cpu:cycle_activity.stalls_l1d_miss"},
+                               {"stalls_l2", "cpu:cycle_activity.stalls_l2_miss"}};
+  add("topdown_l3_L2_bound", "Stalls on L1D misses that hit L2 (Intel); L1D fills by source (Zen)",
+      {{kZen4, fillsZen}, {kZen5, fillsZen}, {kSkx, l2b}, {kIcx, l2b}}, [](const auto& c, double, double, auto& o) {
+        if (c.count("stalls_l1d")) {
+          o["topdown_l2_bound_pct"] =
+              ratio(std::max(0.0, get(c, "stalls_l1d") - get(c, "stalls_l2")), get(c, "cycles")) * 100.0;
+          return;
+        }
+        const double n = get(c, "fills");
+        o["l1d_fill_l2_pct"] = ratio(get(c, "fill_l2"), n) * 100.0;
+        o["l1d_fill_l3_pct"] = ratio(get(c, "fill_l3"), n) * 100.0;
+        o["l1d_fill_remote_cache_pct"] = ratio(get(c, "fill_remote"), n) * 100.0;
+        o["l1d_fill_dram_pct"] = ratio(get(c, "fill_dram"), n) * 100.0;
+      });
   return ms;
 }
 

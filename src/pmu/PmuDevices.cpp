@@ -259,6 +259,8 @@ std::optional<EventConf> genericEvent(const std::string& n) {
       {"cpu-migrations", {PERF_TYPE_SOFTWARE, PERF_COUNT_SW_CPU_MIGRATIONS}},
       {"minor-faults", {PERF_TYPE_SOFTWARE, PERF_COUNT_SW_PAGE_FAULTS_MIN}},
       {"major-faults", {PERF_TYPE_SOFTWARE, PERF_COUNT_SW_PAGE_FAULTS_MAJ}},
+      {"alignment-faults", {PERF_TYPE_SOFTWARE, PERF_COUNT_SW_ALIGNMENT_FAULTS}},
+      {"emulation-faults", {PERF_TYPE_SOFTWARE, PERF_COUNT_SW_EMULATION_FAULTS}},
       {"dummy", {PERF_TYPE_SOFTWARE, PERF_COUNT_SW_DUMMY}},
       // HW cache: (id) | (op << 8) | (result << 16)
       {"L1-dcache-loads", {PERF_TYPE_HW_CACHE, PERF_COUNT_HW_CACHE_L1D | (PERF_COUNT_HW_CACHE_OP_READ << 8) | (PERF_COUNT_HW_CACHE_RESULT_ACCESS << 16)}},
