@@ -99,6 +99,19 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
+def baseline_child_env(environ) -> dict:
+    """Environment of a no-agent child.  Under torchrun the children form
+    their own group on MASTER_PORT + 100, and rank 0's child must host that
+    store itself: torchrun's TORCHELASTIC_USE_AGENT_STORE=True would make
+    every child a client of an agent store that does not exist on that port
+    (all of them would wait for the rendezvous timeout)."""
+    env = dict(environ)
+    if int(env.get("WORLD_SIZE", "1")) > 1:
+        env["MASTER_PORT"] = str(int(env.get("MASTER_PORT", "29511")) + 100)
+        env["TORCHELASTIC_USE_AGENT_STORE"] = "False"
+    return env
+
+
 def run_baseline_child(args, tag: str) -> dict:
     """Times the same workload (model, batch, sequence, optimizer, steps) in a
     child process that never loads the agent: no rocprofiler-sdk tool is
@@ -114,9 +127,7 @@ def run_baseline_child(args, tag: str) -> dict:
            "--micro-batch", str(args.micro_batch), "--seq-len", str(args.seq_len),
            "--optimizer", args.optimizer, "--batches", str(args.batches), "--host-pmu", "off",
            "--no-agent-baseline", "off", "--json-out", path]
-    env = dict(os.environ)
-    if int(env.get("WORLD_SIZE", "1")) > 1:
-        env["MASTER_PORT"] = str(int(env.get("MASTER_PORT", "29511")) + 100)
+    env = baseline_child_env(os.environ)
     t0 = time.time()
     try:
         # the child's stdout goes to stderr: rank 0's stdout carries ONE result line

@@ -156,3 +156,56 @@ def test_agent_index_for_local_rank(env, local_rank, want):
     visible-devices lists (bench.py calls this before HIP initialises)."""
     from dynolog_amd.agent import agent_index_for_local_rank
     assert agent_index_for_local_rank(local_rank, env) == want
+
+
+def test_baseline_child_env_hosts_its_own_store():
+    """bench.py's no-agent children form their own group on MASTER_PORT + 100;
+    under torchrun they must not look for torchrun's agent store there."""
+    import importlib.util
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    env = b.baseline_child_env({"WORLD_SIZE": "8", "MASTER_PORT": "29500", "RANK": "3",
+                                "TORCHELASTIC_USE_AGENT_STORE": "True"})
+    assert env["MASTER_PORT"] == "29600" and env["TORCHELASTIC_USE_AGENT_STORE"] == "False"
+    assert env["RANK"] == "3"
+    one = b.baseline_child_env({"WORLD_SIZE": "1", "MASTER_PORT": "29500"})
+    assert one["MASTER_PORT"] == "29500" and "TORCHELASTIC_USE_AGENT_STORE" not in one
+
+
+_PARENT = r"""
+import importlib.util, os, subprocess, sys
+import torch.distributed as dist
+spec = importlib.util.spec_from_file_location("bench_mod", sys.argv[1])
+b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)
+child = ("import torch, torch.distributed as d; d.init_process_group('gloo'); "
+         "t = torch.ones(1); d.all_reduce(t); assert t.item() == d.get_world_size(); "
+         "d.destroy_process_group()")
+# children first (before the parent group exists), like bench.py's 'before' run
+r = subprocess.run([sys.executable, "-c", child], env=b.baseline_child_env(os.environ), timeout=120)
+dist.init_process_group("gloo")
+dist.barrier()
+# and again while the parent group is up ('after' run)
+r2 = subprocess.run([sys.executable, "-c", child], env=b.baseline_child_env(os.environ), timeout=120)
+dist.barrier()
+print("RC", os.environ["RANK"], r.returncode, r2.returncode, flush=True)
+sys.exit(r.returncode or r2.returncode)
+"""
+
+
+def test_baseline_children_rendezvous_under_torchrun(tmp_path):
+    """The no-agent children of every torchrun rank form their own gloo group
+    on MASTER_PORT + 100 (before and while the parents' group exists).  With
+    torchrun's agent-store flag inherited they would all wait for a store
+    nobody hosts."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "parent.py"
+    script.write_text(_PARENT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29641", str(script), os.path.join(repo, "bench.py")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert sorted(l for l in r.stdout.splitlines() if l.startswith("RC")) == ["RC 0 0 0", "RC 1 0 0"], r.stdout
