@@ -67,7 +67,7 @@ assert AGENT_CONSTS_DTYPE.itemsize == 48
 MI355X_CONSTS = dict(simd_count=1024.0, cu_count=256.0, se_count=32.0, xcc_count=8.0,
                      hbm_read_bytes_per_req=128.0, hbm_read_bytes_per_32b_req=32.0,
                      hbm_write_bytes_per_req=32.0, hbm_write_bytes_per_64b_req=64.0,
-                     valu_fp16_flops_per_clk=128.0, valu_fp32_flops_per_clk=64.0,
+                     valu_fp16_flops_per_clk=64.0, valu_fp32_flops_per_clk=64.0,
                      valu_fp64_flops_per_clk=32.0, pad=0.0)
 
 

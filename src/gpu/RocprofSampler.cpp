@@ -145,10 +145,12 @@ DynoAgentConsts makeAgentConsts(const AgentInfo& a) {
   k.hbm_read_bytes_per_32b_req = 32.0f;
   k.hbm_write_bytes_per_req = 32.0f;
   k.hbm_write_bytes_per_64b_req = 64.0f;
-  // vector-ALU peaks per SIMD per clock on gfx950 (MI355X_MICROARCH: v_fma_f32
-  // wave64 issues in 2 cycles -> 64 FLOP/clk = the 157.3 TF FP32 vector peak;
-  // FP64 at half that, 78.6 TF; packed FP16 v_pk_fma_f16 at twice)
-  k.valu_fp16_flops_per_clk = 128.0f;
+  // vector-ALU peaks per SIMD per clock on gfx950, measured with 8 independent
+  // FMA chains per lane (tools/probes/valu_peak.hip, profiles/round3/g07):
+  // FP32 (the compiler emits v_pk_fma_f32) 59.3, packed FP16 v_pk_fma_f16
+  // 60.3, FP64 28.6 FLOP/clk/SIMD at the 2.4 GHz max sclk -> 64 / 64 / 32
+  // (the 157.3 TF FP32 vector peak; packed FP16 is no faster than FP32)
+  k.valu_fp16_flops_per_clk = 64.0f;
   k.valu_fp32_flops_per_clk = 64.0f;
   k.valu_fp64_flops_per_clk = 32.0f;
   k.pad = 0.0f;
