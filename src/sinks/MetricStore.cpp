@@ -18,7 +18,11 @@ namespace {
 // stream (frame) per distinct combination.
 const char* const kStreamKeys[] = {"device", "phase", "source", "rank", "pid"};
 
-mf::TimePoint tp(int64_t ms) { return mf::TimePoint(std::chrono::milliseconds(ms)); }
+mf::TimePoint tp(int64_t ms) {
+  // open query bounds (INT64_MIN / MAX) clamp to what a ns time point holds
+  constexpr int64_t kLim = std::numeric_limits<int64_t>::max() / 1000000 - 1;
+  return mf::TimePoint(std::chrono::milliseconds(std::clamp<int64_t>(ms, -kLim, kLim)));
+}
 int64_t msOf(mf::TimePoint t) {
   return std::chrono::duration_cast<std::chrono::milliseconds>(t.time_since_epoch()).count();
 }
