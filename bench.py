@@ -318,11 +318,24 @@ def main(argv=None) -> int:
             ag.step()
             torch.cuda.synchronize()
             pdist.barrier()
-            if env.rank == 0:
+            # each gather group's aggregator (job rank 0; with per-node groups
+            # on a multi-node job, every node's first rank) counts its members'
+            # samples inside their own windows
+            mine = None
+            if ag.is_aggregator:
                 ag.flush()
-                per_rank = ag.window_counts([w[0] for w in windows], [w[1] for w in windows])
-                total_samples = sum(per_rank)
-                agent_stats = ag.stats()
+                mw = [windows[r] for r in ag.rank_labels] if len(windows) == env.world else windows
+                mine = list(zip(ag.rank_labels, ag.window_counts([w[0] for w in mw], [w[1] for w in mw])))
+                if env.rank == 0:
+                    agent_stats = ag.stats()
+            if ag.gather_world < env.world and torch.distributed.is_initialized():
+                parts = [None] * env.world
+                torch.distributed.all_gather_object(parts, mine)
+                counts = dict(kv for p in parts if p for kv in p)
+                per_rank = [counts.get(r, 0) for r in range(env.world)] if env.rank == 0 else []
+            elif env.rank == 0:
+                per_rank = [c for _, c in mine]
+            total_samples = sum(per_rank)
             if base_s is not None:
                 # second baseline AFTER the measured window, then --ab-rounds of
                 # interleaved (paused, sampling) window pairs in alternating order.
@@ -423,6 +436,9 @@ def main(argv=None) -> int:
                 if base_s:
                     # the price of the registered-but-paused agent itself
                     out["paused_vs_no_agent_pct"] = round((base_s / args.steps * 1e3 / no_agent_ms - 1.0) * 100.0, 3)
+        if ag is not None:
+            # ranks per gather group (= n_gpus on one node; one group per node otherwise)
+            out["gather_group_size"] = ag.gather_world
         if ag is not None and ag.config.get("fallback_from"):
             out["gather_fallback"] = {"requested": ag.config["fallback_from"],
                                       "reason": ag.config.get("fallback_reason", "")}

@@ -77,6 +77,9 @@ AgentConfig AgentConfig::fromJson(const Json& j) {
   gi("gather_cap_slots", c.gatherCapSlots);
   gi("log_interval_ms", c.logIntervalMs);
   gi("memory_records", c.memoryRecords);
+  gi("job_world", c.jobWorld);
+  if (j.contains("rank_labels"))
+    for (const auto& r : j.at("rank_labels").asArray()) c.rankLabels.push_back(static_cast<int>(r.asInt()));
   if (j.contains("gather_mode")) c.gatherMode = j.at("gather_mode").asString();
   if (j.contains("counter_set")) c.counterSet = j.at("counter_set").asString();
   if (j.contains("counter_passes")) c.counterPasses = j.at("counter_passes").asString();
@@ -183,6 +186,12 @@ bool Agent::setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::st
 bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::string* err) {
   if (running_) {
     *err = "agent already running";
+    return false;
+  }
+  if (cfg.world < 1 || cfg.rank < 0 || cfg.rank >= cfg.world ||
+      (!cfg.rankLabels.empty() && static_cast<int>(cfg.rankLabels.size()) != cfg.world)) {
+    *err = "bad gather group: rank " + std::to_string(cfg.rank) + " of " + std::to_string(cfg.world) + " with " +
+           std::to_string(cfg.rankLabels.size()) + " rank labels";
     return false;
   }
   cfg_ = cfg;
@@ -404,6 +413,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   }
 
   agg_.reset(cfg_.world, cfg_.gatherCapSlots);
+  agg_.setRankLabels(cfg_.rankLabels);
   if (root && !cfg_.slotRing.empty()) {
     // Host ring of the device ring: every slot rank 0
     // receives is re-published, all ranks interleaved, in a lock-free shm ring
@@ -1005,8 +1015,8 @@ bool Agent::writeKernelTrace(const std::string& path, std::string* err) const {
     }
   }
   TraceMeta meta;
-  meta.rank = cfg_.rank;
-  meta.world = cfg_.world;
+  meta.rank = cfg_.jobRank();
+  meta.world = cfg_.jobWorld > 0 ? cfg_.jobWorld : cfg_.world;
   return kt.writeChromeTrace(path, err, &tracks, &meta);
 }
 
@@ -1060,7 +1070,7 @@ void Agent::controlLoop() {
     if (now >= nextKeepalive) {
       Json c = Json::object();
       c["pid"] = pid;
-      c["rank"] = cfg_.rank;
+      c["rank"] = cfg_.jobRank();
       c["device"] = cfg_.device;
       c["endpoint"] = ctl_->endpoint().name();
       c["kernel_trace"] = KernelTracer::get().configured();
@@ -1077,7 +1087,7 @@ void Agent::controlLoop() {
       if (!Json::tryParse(std::string(msg->buf.begin(), msg->buf.end()), &req, &err)) continue;
       res["id"] = req.contains("id") ? req.at("id") : Json(0);
       res["pid"] = pid;
-      res["rank"] = cfg_.rank;
+      res["rank"] = cfg_.jobRank();
       res["device"] = cfg_.device;
       auto& kt = KernelTracer::get();
       const int dur = req.contains("duration_ms") ? static_cast<int>(req.at("duration_ms").asInt()) : 500;
@@ -1340,8 +1350,16 @@ void Agent::releaseDevice() {
 Json Agent::stats() const {
   Json j = Json::object();
   j["running"] = running_.load();
-  j["rank"] = cfg_.rank;
-  j["world"] = cfg_.world;
+  j["rank"] = cfg_.jobRank();
+  j["world"] = cfg_.jobWorld > 0 ? cfg_.jobWorld : cfg_.world;
+  // the gather group (= the job unless gather_scope "node" split a multi-node job)
+  j["gather_rank"] = cfg_.rank;
+  j["gather_world"] = cfg_.world;
+  if (!cfg_.rankLabels.empty()) {
+    Json l = Json::array();
+    for (int r : cfg_.rankLabels) l.push_back(r);
+    j["rank_labels"] = l;
+  }
   j["collective"] = collective_;
   j["device"] = cfg_.device;
   j["sample_hz_target"] = cfg_.sampleHz;

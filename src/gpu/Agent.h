@@ -48,8 +48,14 @@ class ShmGather;
 struct AgentConfig {
   int device = 0;          // HIP device index for this rank
   int agentIndex = -1;     // rocprofiler GPU agent index (-1: match by PCI BDF)
-  int rank = 0;
-  int world = 1;
+  int rank = 0;            // rank in the gather group (the node with gather_scope "node")
+  int world = 1;           // size of the gather group
+  // Job ranks of the gather group's members, by group rank (gather_scope
+  // "node" on a multi-node job: each node gathers to its own first rank).
+  // Empty: the group is the job (labels = group ranks).
+  std::vector<int> rankLabels;
+  int jobWorld = 0;        // ranks in the job (0: = world)
+  int jobRank() const { return rankLabels.empty() ? rank : rankLabels.at(static_cast<size_t>(rank)); }
   double sampleHz = 1000.0;
   int batch = 32;                    // samples per H2D copy + pack launch
   int stages = 64;                   // pinned staging batches in flight (<= 256)

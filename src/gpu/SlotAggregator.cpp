@@ -161,7 +161,7 @@ void SlotAggregator::logInterval(Logger& logger, double sec, uint64_t monoNowNs)
     else
       logger.setTimestamp(wallNow);
     logger.logInt("device", a.device >= 0 ? a.device : r);
-    logger.logInt("rank", r);
+    logger.logInt("rank", rankLabel(r));
     logger.logUint("counter_samples", a.intervalSamples);
     logger.logFloat("counter_sample_rate_hz", static_cast<float>(rate));
     logger.logFloat("sample_latency_us", static_cast<float>(a.latencySumNs / n * 1e-3));
@@ -208,7 +208,7 @@ void SlotAggregator::logInterval(Logger& logger, double sec, uint64_t monoNowNs)
         if (ph.intervalSamples == 0) continue;
         logger.setTimestamp(wallNow);
         logger.logInt("device", a.device >= 0 ? a.device : r);
-        logger.logInt("rank", r);
+        logger.logInt("rank", rankLabel(r));
         logger.logStr("phase", phaseName(id));
         logger.logUint("counter_samples", ph.intervalSamples);
         for (int d = 0; d < DD_NUM_DERIVED; ++d)

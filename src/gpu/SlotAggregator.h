@@ -112,6 +112,12 @@ class SlotAggregator {
   void logInterval(Logger& logger, double intervalSec, uint64_t monoNowNs = 0);
 
   void setPhaseName(uint32_t id, const std::string& name) { phaseNames_[id] = name; }
+  // Job rank of each group rank, for the records' "rank" key (per-node
+  // gathers of a multi-node job); empty = the group rank itself.
+  void setRankLabels(std::vector<int> labels) { rankLabels_ = std::move(labels); }
+  int rankLabel(int r) const {
+    return r >= 0 && static_cast<size_t>(r) < rankLabels_.size() ? rankLabels_[static_cast<size_t>(r)] : r;
+  }
   std::string phaseName(uint32_t id) const;
   Json phaseStats() const;
   Json rankStats() const;  // [{received, dropped, last_seq}] per rank
@@ -129,6 +135,7 @@ class SlotAggregator {
  private:
   std::vector<RankAggregate> ranks_;
   std::map<uint32_t, std::string> phaseNames_;
+  std::vector<int> rankLabels_;
   uint32_t capSlots_ = 0;
   size_t histCap_ = size_t(1) << 17;
 };

@@ -535,3 +535,35 @@ TEST(GpuHost, CounterPassesAggregatePerMetric) {
   // counter tracks keep the main pass only (every track metric is valid there)
   EXPECT_EQ(agg.counterTrackEvents(0, UINT64_MAX, 1).size(), 3u * 5u);
 }
+
+// Per-node gather groups of a multi-node job (gather_scope "node"): the
+// node's aggregator receives group ranks 0..3 and logs them under their job
+// ranks (node 1 of a 2 x 4 job: job ranks 4..7), with the GPU from the headers.
+TEST(GpuHost, NodeGroupRecordsCarryJobRanks) {
+  SlotAggregator agg;
+  agg.reset(4, 64);
+  agg.setRankLabels({4, 5, 6, 7});
+  EXPECT_EQ(agg.rankLabel(2), 6);
+  EXPECT_EQ(agg.rankLabel(9), 9);  // out of range: the group rank itself
+  auto store = std::make_shared<MemoryLogger::Store>();
+  MemoryLogger ml(store);
+  std::vector<DynoSlot> slots(10);
+  for (int r = 0; r < 4; ++r) {
+    for (size_t i = 0; i < slots.size(); ++i) {
+      slots[i] = DynoSlot{};
+      slots[i].seq = i;
+      slots[i].host_ts_ns = 1'000'000'000ull + i * 1'000'000ull;
+    }
+    DynoGatherHeader h{};
+    h.count = static_cast<uint32_t>(slots.size());
+    h.rank = static_cast<uint32_t>(r);
+    h.device = r;  // local GPU index on this node
+    agg.ingestRank(r, h, slots.data());
+  }
+  agg.logInterval(ml, 1.0, 1'010'000'000ull);
+  ASSERT_EQ(store->records.size(), 4u);
+  for (int r = 0; r < 4; ++r) {
+    EXPECT_EQ(static_cast<int>(num(store->records[static_cast<size_t>(r)], "rank")), 4 + r);
+    EXPECT_EQ(static_cast<int>(num(store->records[static_cast<size_t>(r)], "device")), r);
+  }
+}

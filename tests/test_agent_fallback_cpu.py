@@ -209,3 +209,20 @@ def test_baseline_children_rendezvous_under_torchrun(tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert sorted(l for l in r.stdout.splitlines() if l.startswith("RC")) == ["RC 0 0 0", "RC 1 0 0"], r.stdout
+
+
+def test_plan_gather_group_per_node():
+    """gather_scope 'node': on a 2-node job every node's ranks form their own
+    gather group (led by the node's first rank); on one node it is the job."""
+    from dynolog_amd.agent import plan_gather_group
+    hosts = ["a"] * 4 + ["b"] * 4
+    assert plan_gather_group(0, 8, hosts) == (0, 4, [0, 1, 2, 3])
+    assert plan_gather_group(6, 8, hosts) == (2, 4, [4, 5, 6, 7])
+    assert plan_gather_group(6, 8, hosts, "job") == (6, 8, None)
+    assert plan_gather_group(3, 8, ["a"] * 8) == (3, 8, None)
+    # interleaved placement (rank r on node r % 2)
+    inter = ["a", "b"] * 4
+    assert plan_gather_group(5, 8, inter) == (2, 4, [1, 3, 5, 7])
+    assert plan_gather_group(0, 1, ["a"]) == (0, 1, None)
+    with pytest.raises(ValueError):
+        plan_gather_group(0, 2, ["a", "a"], "rack")
