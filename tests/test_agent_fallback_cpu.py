@@ -189,7 +189,8 @@ dist.barrier()
 # and again while the parent group is up ('after' run)
 r2 = subprocess.run([sys.executable, "-c", child], env=b.baseline_child_env(os.environ), timeout=120)
 dist.barrier()
-print("RC", os.environ["RANK"], r.returncode, r2.returncode, flush=True)
+with open(os.path.join(sys.argv[2], "rc_" + os.environ["RANK"]), "w") as f:
+    f.write(f"{r.returncode} {r2.returncode}")
 sys.exit(r.returncode or r2.returncode)
 """
 
@@ -205,10 +206,12 @@ def test_baseline_children_rendezvous_under_torchrun(tmp_path):
     script = tmp_path / "parent.py"
     script.write_text(_PARENT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29641", str(script), os.path.join(repo, "bench.py")]
+           "--master-addr=127.0.0.1", "--master-port=29641", str(script), os.path.join(repo, "bench.py"),
+           str(tmp_path)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    assert sorted(l for l in r.stdout.splitlines() if l.startswith("RC")) == ["RC 0 0 0", "RC 1 0 0"], r.stdout
+    for rank in (0, 1):  # both children of both ranks exited cleanly
+        assert (tmp_path / f"rc_{rank}").read_text() == "0 0"
 
 
 def test_plan_gather_group_per_node():

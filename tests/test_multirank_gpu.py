@@ -5,6 +5,7 @@ loop with every fused CDNA4 kernel (`small` config: head_dim 128), FusedAdamW
 and the per-rank counter agents.  Checks the single JSON line rank 0 prints."""
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -120,5 +121,5 @@ def test_per_node_gather_groups_rehearsal(native_built):
     per = out["samples_per_rank"]
     assert len(per) == 4 and all(n > 0 for n in per), per
     # both aggregators logged records, each under its members' job ranks
-    logged = {int(m) for m in __import__("re").findall(r'"rank":\s*"?(\d+)', r.stderr)}
+    logged = {int(m) for m in re.findall(r'"rank":\s*"?(\d+)', r.stderr)}
     assert {0, 1, 2, 3} <= logged, sorted(logged)
