@@ -8,7 +8,9 @@
 // (MFMA-busy share, bf16 FLOP/s, HBM read / write bytes/s, GPU-busy share) is
 // additive over time: for sample i,
 //     amount_i = rate_i * dt_i = sum_k overlap(i, k) * x_k + idle_i * x_idle
-// with overlap(i, k) the ns kernel class k ran inside the interval.  Solving
+// with overlap(i, k) the ns kernel class k ran inside the interval.  With
+// rotating counter passes a sample measures only its pass's metrics
+// (KcSample::valid); each metric is fitted over the samples that carry it.  Solving
 // this for x >= 0 over thousands of samples (non-negative least squares on
 // the K x K normal equations, K = kernel classes seen) de-mixes the
 // classes: x_k is the counter rate while class k runs.  rocprofv3 --pmc gets
@@ -34,8 +36,15 @@ enum KcMetric {
   KC_TFLOPS,        // bf16 MFMA TFLOP/s
   KC_HBM_READ,      // GB/s
   KC_HBM_WRITE,     // GB/s
+  KC_VALU_FP32,     // vector-ALU fp32 TFLOP/s (precision counter pass only)
+  KC_VALU_FP64,     // vector-ALU fp64 TFLOP/s (precision pass)
+  KC_VALU_FP16,     // vector-ALU fp16 TFLOP/s (precision pass)
   KC_NUM
 };
+// metrics every sample carries / the main pass adds / the precision pass adds
+constexpr uint32_t kKcCommon = (1u << KC_BUSY) | (1u << KC_TFLOPS) | (1u << KC_HBM_READ) | (1u << KC_HBM_WRITE);
+constexpr uint32_t kKcMainPass = kKcCommon | (1u << KC_MFMA);
+constexpr uint32_t kKcPrecisionPass = kKcCommon | (1u << KC_VALU_FP32) | (1u << KC_VALU_FP64) | (1u << KC_VALU_FP16);
 const char* kcMetricName(int m);
 
 struct KcSpan {
@@ -46,6 +55,7 @@ struct KcSpan {
 struct KcSample {
   uint64_t t0 = 0, t1 = 0;  // interval the counter deltas cover
   double v[KC_NUM] = {};    // rates over the interval (units of KcMetric)
+  uint32_t valid = kKcMainPass;  // metrics this sample measured (its counter pass)
 };
 
 struct KcClassResult {
@@ -62,6 +72,7 @@ struct KcResult {
   double idleRate[KC_NUM] = {};        // estimated rates while no traced kernel runs
   double r2[KC_NUM] = {};              // fit quality per metric
   size_t samples = 0;
+  size_t metricSamples[KC_NUM] = {};   // samples that measured each metric (0: not fitted)
 };
 
 // minCoverNs: classes whose total overlap is below this are not solved for

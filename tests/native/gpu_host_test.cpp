@@ -532,8 +532,21 @@ TEST(GpuHost, CounterPassesAggregatePerMetric) {
   EXPECT_NEAR(last.at("mfma_util").asDouble(), 30.0, 1e-4);   // from the newest main-pass slot
   EXPECT_NEAR(last.at("fp32_active").asDouble(), 0.25, 1e-6);
   EXPECT_NEAR(last.at("gpu_busy_pct").asDouble(), 80.0, 1e-4);  // the newest slot overall
-  // counter tracks keep the main pass only (every track metric is valid there)
-  EXPECT_EQ(agg.counterTrackEvents(0, UINT64_MAX, 1).size(), 3u * 5u);
+  // counter tracks: every slot's own metrics (3 main-pass slots with MFMA
+  // utilisation, the precision slot with vector TFLOP/s instead)
+  const auto tracks = agg.counterTrackEvents(0, UINT64_MAX, 1);
+  EXPECT_EQ(tracks.size(), 4u * 5u);
+  int mfma = 0, valu = 0;
+  for (const auto& e : tracks) {
+    const std::string n = e.at("name").asString();
+    if (n == "gpu0 mfma_util_pct") ++mfma;
+    if (n == "gpu0 valu_tflops") {
+      ++valu;
+      EXPECT_NEAR(e.at("args").at("fp32").asDouble(), 2.0, 1e-4);
+    }
+  }
+  EXPECT_EQ(mfma, 3);
+  EXPECT_EQ(valu, 1);
 }
 
 // Per-node gather groups of a multi-node job (gather_scope "node"): the
@@ -566,4 +579,53 @@ TEST(GpuHost, NodeGroupRecordsCarryJobRanks) {
     EXPECT_EQ(static_cast<int>(num(store->records[static_cast<size_t>(r)], "rank")), 4 + r);
     EXPECT_EQ(static_cast<int>(num(store->records[static_cast<size_t>(r)], "device")), r);
   }
+}
+
+// Rotating counter passes in a kernel trace window: 3 of every 4 samples
+// measure the main set (MFMA busy), 1 the precision set (vector fp32/fp64/
+// fp16 TFLOP/s); each metric is fitted over the samples that carry it.  An
+// elementwise fp32 class, an fp64 class and a GEMM class alternate.
+TEST(GpuHost, KernelCountersAcrossCounterPasses) {
+  //                         busy mfma  bf16   hbm_r  hbm_w  fp32  fp64  fp16
+  const KcTruth truth[3] = {{{100, 0, 0, 2000, 2000, 40, 0, 0}},
+                            {{100, 0, 0, 300, 100, 0, 60, 0}},
+                            {{100, 70, 1400, 300, 50, 0.5, 0, 0}}};
+  std::vector<KcSpan> spans;
+  const uint64_t T0 = 1000000000ull;
+  uint64_t t = T0;
+  while (t < T0 + 4000000000ull) {
+    spans.push_back({t, t + 300000, 0});
+    t += 330000;
+    spans.push_back({t, t + 250000, 1});
+    t += 280000;
+    spans.push_back({t, t + 450000, 2});
+    t += 470000;
+  }
+  auto samples = kcSamplesFor(spans, truth, T0, t, 1000000, 0.0);
+  for (size_t i = 0; i < samples.size(); ++i) {
+    auto& s = samples[i];
+    if (i % 4 == 3) {
+      s.valid = kKcPrecisionPass;
+      s.v[KC_MFMA] = 0;  // not measured by this pass
+    } else {
+      s.valid = kKcMainPass;
+      s.v[KC_VALU_FP32] = s.v[KC_VALU_FP64] = s.v[KC_VALU_FP16] = 0;
+    }
+  }
+  KcResult r = attributeCounters(spans, 3, samples);
+  EXPECT_EQ(r.metricSamples[KC_MFMA], samples.size() - samples.size() / 4);
+  EXPECT_EQ(r.metricSamples[KC_VALU_FP32], samples.size() / 4);
+  EXPECT_EQ(r.metricSamples[KC_BUSY], samples.size());
+  for (int c = 0; c < 3; ++c) {
+    ASSERT_TRUE(r.classes[static_cast<size_t>(c)].solved);
+    for (int m = 0; m < KC_NUM; ++m) {
+      const double want = truth[c].r[m], got = r.classes[static_cast<size_t>(c)].rate[m];
+      EXPECT_LE(std::fabs(got - want), 0.01 * std::max(want, 10.0));
+    }
+  }
+  EXPECT_GT(r.r2[KC_VALU_FP32], 0.99);
+  EXPECT_GT(r.r2[KC_MFMA], 0.99);
+  // without per-metric masks the zeros of the other pass would drag the
+  // estimates: the precision-pass zeros for MFMA would cut the GEMM's 70 %
+  EXPECT_GT(r.classes[2].rate[KC_MFMA], 69.0);
 }
