@@ -3,6 +3,7 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -326,6 +327,71 @@ void registerPluginRpcs(rpc::RpcDispatcher& disp, Daemon& d) {
     std::string e;
     if (!Json::tryParse(out, &j, &e)) j = Json::object();
     j["status"] = "ok";
+    return j;
+  });
+  // the always-on shared counters (--shared_counters, --shared_counters_cgroups)
+  // as any reader sees them: totals, or rates over `interval_ms` (<= 10 s)
+  disp.addLong("getSharedCounters", [](const Json& req) -> std::optional<Json> {
+    Json j = Json::object();
+    std::string err;
+    auto sys = pmu::SharedCounterReader::open(FLAGS_shared_counters_shm, &err);
+    if (!sys) {
+      j["status"] = "disabled (start dynolog with --shared_counters EVENTS): " + err;
+      return j;
+    }
+    auto cg = pmu::SharedCgroupCounterReader::open(FLAGS_shared_counters_shm + "_cgroups", &err);
+    const int64_t ms = req.contains("interval_ms") ? std::clamp<int64_t>(req.at("interval_ms").asInt(), 0, 10000) : 0;
+    auto a = sys->read();
+    auto ca = cg ? cg->read() : std::nullopt;
+    if (!a) {
+      j["status"] = "failed: no consistent snapshot";
+      return j;
+    }
+    if (ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+    auto b = ms > 0 ? sys->read() : a;
+    auto cb = ms > 0 && cg ? cg->read() : ca;
+    if (!b) b = a;
+    const double sec = b->updateNs > a->updateNs ? (b->updateNs - a->updateNs) * 1e-9 : 0.0;
+    auto vec = [](const std::vector<double>& v) {
+      Json x = Json::array();
+      for (double d : v) x.push_back(d);
+      return x;
+    };
+    auto rates = [&](const std::vector<double>& x, const std::vector<double>& y) {
+      Json r = Json::array();
+      for (size_t i = 0; i < x.size() && i < y.size(); ++i) r.push_back(sec > 0 ? (y[i] - x[i]) / sec : 0.0);
+      return r;
+    };
+    Json names = Json::array();
+    for (const auto& n : b->names) names.push_back(n);
+    j["status"] = "ok";
+    j["events"] = names;
+    j["system_total"] = vec(b->total());
+    if (ms > 0) {
+      j["interval_s"] = sec;
+      j["system_per_s"] = rates(a->total(), b->total());
+    }
+    if (cb) {
+      Json cgs = Json::array();
+      for (size_t t = 0; t < cb->paths.size(); ++t) {
+        Json c = Json::object();
+        c["path"] = cb->paths[t];
+        c["total"] = vec(cb->perTarget[t]);
+        if (ms > 0 && ca && t < ca->perTarget.size()) {
+          const double csec = cb->updateNs > ca->updateNs ? (cb->updateNs - ca->updateNs) * 1e-9 : 0.0;
+          Json r = Json::array();
+          for (size_t i = 0; i < cb->perTarget[t].size() && i < ca->perTarget[t].size(); ++i)
+            r.push_back(csec > 0 ? (cb->perTarget[t][i] - ca->perTarget[t][i]) / csec : 0.0);
+          c["per_s"] = r;
+        }
+        cgs.push_back(c);
+      }
+      Json cn = Json::array();
+      for (const auto& n : cb->names) cn.push_back(n);
+      j["cgroup_events"] = cn;  // the switch-count leader first, then the shared events
+      j["cgroups"] = cgs;
+      j["cgroup_slices"] = static_cast<unsigned long long>(cb->slices);
+    }
     return j;
   });
   disp.addLong("cpuTrace", rpc::asyncCapable(d.jobs(), "cpuTrace",

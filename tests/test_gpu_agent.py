@@ -14,8 +14,9 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(code: str, timeout=240):
+def _run(code: str, timeout=240, extra_env=None):
     env = dict(os.environ)
+    env.update(extra_env or {})
     env["PYTHONPATH"] = REPO + os.pathsep + env.get("PYTHONPATH", "")
     r = subprocess.run([sys.executable, "-c", textwrap.dedent(code)], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=timeout)
@@ -550,3 +551,30 @@ def test_precision_pass_separates_vector_and_matrix_work(native_built):
     # interval records carry the DCGM keys and per-precision rates
     rec = [r for r in res["recs"] if "fp32_active" in r]
     assert rec and "valu_fp32_tflops" in rec[-1] and "mfma_f32_tflops" in rec[-1], res["recs"]
+
+
+def test_agent_index_under_visible_devices(native_built):
+    """With HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES set (a scheduler's
+    per-job GPU list), the rank's HIP device 0 maps to its rocprofiler agent
+    through the lists (agent_index_for_local_rank), so preinit() creates one
+    counting context, for that GPU only, and the agent samples it."""
+    res = _run("""
+        import os
+        from dynolog_amd import agent
+        idx = agent.agent_index_for_local_rank(0)
+        agent.preinit([idx])
+        import json, time, torch
+        torch.cuda.set_device(0)
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), log_interval_ms=200)
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        end = time.time() + 1.0
+        while time.time() < end:
+            y = x @ x
+            a.step()
+        torch.cuda.synchronize(); a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+        st = a.stats(); a.stop()
+        print("RESULT " + json.dumps(dict(idx=idx, n=torch.cuda.device_count(), st=st)))
+    """, extra_env={"HIP_VISIBLE_DEVICES": "0", "ROCR_VISIBLE_DEVICES": "0"})
+    assert res["idx"] == 0 and res["n"] == 1, res
+    st = res["st"]
+    assert st["samples_taken"] > 500 and st["samples_failed"] == 0 and st["last_error"] == "", st
