@@ -475,3 +475,14 @@ def test_host_pmu_summary_survives_dead_daemon(native_built):
     assert sm["status"] == "failed" and "records" in sm["reason"]
     s.set_enabled(False)  # no raise either
     s.stop()
+
+
+def test_reference_dcgm_flags_are_accepted(native_built, tmp_path):
+    """An existing dynolog flagfile with the DCGM flags keeps working: the
+    daemon starts and answers (the flags are accepted; --dcgm_fields maps onto
+    the counter monitor's passes when that monitor is enabled)."""
+    ff = tmp_path / "dynolog.gflags"
+    ff.write_text("--dcgm_fields=100,155,204,1001,1002,1003,1004,1005,1006,1007,1008\n"
+                  "--dcgm_lib_path=/lib64/libdcgm.so\n--dcgm_major_version=2\n--dcgm_reporting_interval_s=10\n")
+    with DaemonProcess([f"--flagfile={ff}"]) as d:
+        assert d.rpc({"fn": "getStatus"})["status"] == 1
