@@ -449,7 +449,8 @@ def main(argv=None) -> int:
                              "gathers", "raw_instances", "last_error", "gather_latency_us_avg",
                              "gather_latency_us_max", "gather_latency_samples", "gather_bytes",
                              "gather_slots", "gather_cap_slots_now", "gather_backlog", "drain_bytes",
-                             "counter_passes", "pass_switches", "pass_switch_us_avg")
+                             "counter_passes", "pass_switches", "pass_switch_us_avg",
+                             "sampler_cpu_pct", "consumer_cpu_pct")
                             if k in agent_stats}
         if args.host_pmu != "off":
             # one co-sampler per node (local rank 0): every node's summary

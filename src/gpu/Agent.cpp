@@ -559,7 +559,16 @@ void Agent::switchPass() {
   passSwitchNs_ += t2 - t0;
 }
 
+namespace {
+// CPU time of a thread of this process (its clock id from pthread_getcpuclockid)
+double threadCpuSec(clockid_t c) {
+  timespec ts{};
+  return clock_gettime(c, &ts) == 0 ? ts.tv_sec + ts.tv_nsec * 1e-9 : 0.0;
+}
+}  // namespace
+
 void Agent::samplerLoop() {
+  if (pthread_getcpuclockid(pthread_self(), &samplerClock_) == 0) samplerClockValid_ = true;
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
   uint64_t next = monoNs();
   int staged = 0;
@@ -893,6 +902,7 @@ bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err
 }
 
 void Agent::consumerLoop() {
+  if (pthread_getcpuclockid(pthread_self(), &consumerClock_) == 0) consumerClockValid_ = true;
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
   while (true) {
     int slot = -1;
@@ -1272,6 +1282,7 @@ void Agent::stop() {
   if (!running_) return;
   stopFlag_ = true;
   cv_.notify_all();
+  samplerClockValid_ = consumerClockValid_ = false;  // the clock ids die with the threads
   if (samplerThread_.joinable()) samplerThread_.join();
   if (consumerThread_.joinable()) consumerThread_.join();
   if (ctlThread_.joinable()) ctlThread_.join();
@@ -1434,7 +1445,13 @@ Json Agent::stats() const {
     j["pass_switches"] = static_cast<unsigned long long>(sw);
     j["pass_switch_us_avg"] = sw ? passSwitchNs_.load() / static_cast<double>(sw) * 1e-3 : 0.0;
   }
-  j["elapsed_s"] = running_ ? (monoNs() - startNs_) * 1e-9 : 0.0;
+  const double el = running_ ? (monoNs() - startNs_) * 1e-9 : 0.0;
+  j["elapsed_s"] = el;
+  // host cost of the agent's own threads (share of one CPU since start)
+  if (running_ && el > 0) {
+    if (samplerClockValid_) j["sampler_cpu_pct"] = 100.0 * threadCpuSec(samplerClock_) / el;
+    if (consumerClockValid_) j["consumer_cpu_pct"] = 100.0 * threadCpuSec(consumerClock_) / el;
+  }
   j["last_error"] = lastError_;
   if (sampler_) j["agent"] = sampler_->agent().name;
   if (cfg_.rank == 0) {

@@ -276,6 +276,8 @@ class Agent {
       gathers_{0}, latencySumNs_{0}, latencyMaxNs_{0}, lateTicks_{0};
   std::string lastError_;
   uint64_t startNs_ = 0;
+  clockid_t samplerClock_{}, consumerClock_{};  // per-thread CPU clocks (stats)
+  std::atomic<bool> samplerClockValid_{false}, consumerClockValid_{false};
   std::string pinnedCpus_;
   uint32_t* hPhase_ = nullptr;                  // GPU-written current phase (coherent pinned)
   std::unique_ptr<ring::ShmRing<>> slotRing_;   // raw slot export (consumer thread)
