@@ -694,6 +694,14 @@ bool Agent::step(hipStream_t stream, std::string* err) {
   std::lock_guard<std::mutex> g(stepMu_);
   steps_++;
   if (paused_) return true;  // every rank pauses at the same program point
+  // Inside a hipGraph capture the gather would be frozen with this step's
+  // ring range and payload size and replayed stale: skip it (call step()
+  // outside the captured region; the slots wait in the device ring).
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
+    captureSkips_++;
+    return true;
+  }
   if (cfg_.gatherMode == "none" && cfg_.world > 1) return true;
   if (gatherFailed_) return true;  // degraded: keep sampling locally, never block training
   // Failure detection on the metrics path: an RCCL async error (peer lost,
@@ -1408,6 +1416,7 @@ Json Agent::stats() const {
   j["gather_cap_slots_now"] = static_cast<unsigned long long>(capNow_.load());
   j["gather_backlog"] = static_cast<unsigned long long>(backlogNow_.load());
   j["gather_run_ahead_waits"] = static_cast<unsigned long long>(runAheadWaits_.load());
+  j["steps_skipped_in_graph_capture"] = static_cast<unsigned long long>(captureSkips_.load());
   // trainer-stream time of a gather (gather_prep + size all-reduce + collective)
   const uint64_t nt = gatherTimed_.load();
   j["gather_latency_samples"] = static_cast<unsigned long long>(nt);

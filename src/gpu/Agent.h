@@ -231,6 +231,7 @@ class Agent {
   uint32_t recvCap_[kRecv] = {};        // payload cap of the gather in each recv buffer
   std::atomic<uint64_t> gatherBytes_{0}, gatherSlots_{0}, drainBytes_{0}, runAheadWaits_{0};
   std::atomic<uint64_t> backlogNow_{0}, capNow_{0};
+  std::atomic<uint64_t> captureSkips_{0};  // step() calls inside a hipGraph capture
   bool gatherCollective(hipStream_t stream, uint64_t head, std::string* err);
   bool gatherLocal(hipStream_t stream, uint64_t head, std::string* err);
 

@@ -580,3 +580,37 @@ def test_agent_index_under_visible_devices(native_built):
     assert res["idx"] == 0 and res["n"] == 1, res
     st = res["st"]
     assert st["samples_taken"] > 500 and st["samples_failed"] == 0 and st["last_error"] == "", st
+
+
+def test_step_inside_graph_capture_is_skipped(native_built):
+    """A training step captured in a hipGraph (torch.cuda.graph) that calls
+    step() inside the capture: the gather is not frozen into the graph (it
+    would replay a stale ring range); the call is counted and skipped, and
+    the next step() outside the graph delivers every slot."""
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit()
+        import json, time, torch
+        torch.cuda.set_device(0)
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            y = x @ x
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            y = x @ x
+            a.step()
+        end = time.time() + 1.0
+        while time.time() < end:
+            g.replay()
+        torch.cuda.synchronize()
+        a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+        st = a.stats(); a.stop()
+        print("RESULT " + json.dumps(st))
+    """)
+    assert res["steps_skipped_in_graph_capture"] == 1, res
+    assert res["last_error"] == "" and res["samples_failed"] == 0, res
+    assert res["ranks"][0]["received"] > 500, res
