@@ -368,10 +368,14 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
                              collective_ ? hipHostMallocCoherent : hipHostMallocDefault),
                "hipHostMalloc recv");
       }
-      HIP_OK(hipEventCreateWithFlags(&gathered_[i], hipEventDisableTiming), "event");
-      HIP_OK(hipEventCreateWithFlags(&drained_[i], hipEventDisableTiming), "event");
-      recvUsed_[i] = false;
     }
+  }
+  // every rank records a gather event per step (a collective non-root rank
+  // has no receive buffer but orders its agreement copy after the gather)
+  for (int i = 0; i < kRecv; ++i) {
+    HIP_OK(hipEventCreateWithFlags(&gathered_[i], hipEventDisableTiming), "event");
+    HIP_OK(hipEventCreateWithFlags(&drained_[i], hipEventDisableTiming), "event");
+    recvUsed_[i] = false;
   }
   if (collective_) {
     HIP_OK(hipMalloc(&dAgree_, 2 * kAgree * sizeof(uint64_t)), "hipMalloc agree");
@@ -789,7 +793,6 @@ bool Agent::gatherLocal(hipStream_t stream, uint64_t head, std::string* err) {
     // so the trainer's stream never waits on the host
     const int slot = recvNext_;
     recvNext_ = (recvNext_ + 1) % kRecv;
-    if (!gathered_[slot]) HIP_OK(hipEventCreateWithFlags(&gathered_[slot], hipEventDisableTiming), "event");
     HIP_OK(hipEventRecord(gathered_[slot], stream), "record gathered");
     HIP_OK(hipStreamWaitEvent(drainStream_, gathered_[slot], 0), "wait gathered");
     struct Pub {
