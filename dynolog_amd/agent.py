@@ -263,7 +263,7 @@ class GpuAgent:
               daemon_endpoint: str = "dynolog", fault_inject: str = "",
               slot_ring: str = "", stages: int = 64,
               force_collective: bool = False, counter_passes: str = "",
-              gather_scope: str = "node") -> "GpuAgent":
+              gather_scope: str = "node", force_collective_role: str = "") -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
@@ -321,6 +321,8 @@ class GpuAgent:
             cfg["job_world"] = world
         if force_collective:  # testing: RCCL gather path with a 1-rank communicator
             cfg["force_collective"] = True
+            if force_collective_role:  # "nonroot": run it as a gather member, not the root
+                cfg["force_collective_role"] = force_collective_role
         if fault_inject:  # testing: "gather_error@N"
             cfg["fault_inject"] = fault_inject
         if slot_ring:  # rank 0: raw slot stream in /dev/shm (utils/slot_ring.py)

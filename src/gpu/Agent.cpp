@@ -87,6 +87,7 @@ AgentConfig AgentConfig::fromJson(const Json& j) {
   if (j.contains("daemon_endpoint")) c.daemonEndpoint = j.at("daemon_endpoint").asString();
   if (j.contains("pin_threads")) c.pinThreads = j.at("pin_threads").asBool();
   if (j.contains("force_collective")) c.forceCollective = j.at("force_collective").asBool();
+  if (j.contains("force_collective_role")) c.forceNonRoot = j.at("force_collective_role").asString() == "nonroot";
   if (j.contains("slot_ring")) c.slotRing = j.at("slot_ring").asString();
   gi("slot_ring_bytes", c.slotRingBytes);
   if (j.contains("fault_inject")) {
@@ -192,6 +193,10 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
       (!cfg.rankLabels.empty() && static_cast<int>(cfg.rankLabels.size()) != cfg.world)) {
     *err = "bad gather group: rank " + std::to_string(cfg.rank) + " of " + std::to_string(cfg.world) + " with " +
            std::to_string(cfg.rankLabels.size()) + " rank labels";
+    return false;
+  }
+  if (cfg.forceNonRoot && !(cfg.forceCollective && cfg.world == 1)) {
+    *err = "force_collective_role nonroot is a 1-rank test mode (needs force_collective at world 1)";
     return false;
   }
   cfg_ = cfg;
@@ -352,7 +357,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
 
   sendBytes_ = gatherBlockBytes(cfg_.gatherCapSlots);
   HIP_OK(hipMalloc(&dSend_, sendBytes_), "hipMalloc send");
-  const bool root = cfg_.rank == 0;
+  const bool root = cfg_.isRoot();
   // shm mode: rank 0 drains only its own block; the peers' come through the mailbox
   const size_t recvBytes = shmMode_ ? (root ? sendBytes_ : 0)
                            : (cfg_.gatherMode == "allgather" || root) ? sendBytes_ * static_cast<size_t>(cfg_.world)
@@ -774,7 +779,7 @@ void Agent::harvestGatherTimers() {
 bool Agent::gatherLocal(hipStream_t stream, uint64_t head, std::string* err) {
   (void)err;
   const auto rg = planGatherRange(head, gatheredHost_, cfg_.gatherCapSlots, cfg_.ringSlots);
-  if (shmMode_ && cfg_.rank != 0) {
+  if (shmMode_ && !cfg_.isRoot()) {
     uint8_t* blk = shm_->reserve(cfg_.rank, shmEnq_);
     if (!blk) {
       // rank 0 is behind: keep the slots in the device ring for the next step
@@ -864,7 +869,7 @@ bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err
   const auto rg = planGatherRange(head, gatheredHost_, cap, cfg_.ringSlots);
   const size_t block = gatherBlockBytes(cap);
   const int e = static_cast<int>(g % kAgree);
-  const bool root = cfg_.rank == 0;
+  const bool root = cfg_.isRoot();
   const int slot = recvNext_;
   uint8_t* recv = dRecv_[slot];
   if (recv && recvUsed_[slot]) HIP_OK(hipStreamWaitEvent(stream, drained_[slot], 0), "wait drain");
@@ -878,6 +883,7 @@ bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err
     return false;
   }
   if (cfg_.gatherMode == "allgather") r = ncclAllGather(dSend_, recv, block, ncclUint8, comm_, stream);
+  else if (cfg_.forceNonRoot) r = ncclGather(dSend_, dSend_, block, ncclUint8, 0, comm_, stream);  // 1-rank test: in place
   else r = ncclGather(dSend_, root ? recv : nullptr, block, ncclUint8, 0, comm_, stream);
   if (r != ncclSuccess) {
     if (err) *err = std::string(cfg_.gatherMode == "allgather" ? "ncclAllGather: " : "ncclGather: ") +
@@ -1005,7 +1011,7 @@ void Agent::waitSamplesThrough(uint64_t t1) const {
   // the window's last samples reach rank 0 with the next step()'s gather:
   // give the training loop up to 1 s to deliver them
   const uint64_t deadline = monoNs() + 1000000000ull;
-  while (cfg_.rank == 0 && running_ && !paused_ && monoNs() < deadline) {
+  while (cfg_.isRoot() && running_ && !paused_ && monoNs() < deadline) {
     {
       std::lock_guard<std::mutex> lk(aggMu_);
       uint64_t oldest = UINT64_MAX;
@@ -1050,7 +1056,7 @@ void Agent::flush() {
   std::unique_lock<std::mutex> lk(aggMu_);
   condWaitFor(flushCv_, lk, std::chrono::seconds(30), [&] {
     if (inFlight_ != 0) return false;
-    if (shmMode_ && cfg_.rank == 0)
+    if (shmMode_ && cfg_.isRoot())
       for (int r = 1; r < cfg_.world; ++r)
         if (shm_->consumed(r) < shm_->published(r)) return false;
     return true;
@@ -1121,7 +1127,7 @@ void Agent::controlLoop() {
         kt.stop(&err);
         res["status"] = "ok";
         res["summary"] = kt.summary(static_cast<size_t>(std::max(top, 1)));
-        if (cfg_.rank == 0 && !paused_) {
+        if (cfg_.isRoot() && !paused_) {
           // per-kernel counters from this window's 1 kHz samples (KernelCounters)
           packPending();
           waitSamplesThrough(kt.window().second);
@@ -1133,7 +1139,7 @@ void Agent::controlLoop() {
         if (req.contains("chrome_path") && req.at("chrome_path").isString()) {
           const std::string path = req.at("chrome_path").asString();
           // flush pending samples so the counter tracks cover the window
-          if (cfg_.rank == 0 && !paused_) packPending();
+          if (cfg_.isRoot() && !paused_) packPending();
           if (writeKernelTrace(path, &err)) res["chrome_path"] = path;
           else res["chrome_error"] = err;
         }
@@ -1144,7 +1150,7 @@ void Agent::controlLoop() {
 }
 
 Json Agent::kernelCounters(size_t top, std::string* err) const {
-  if (cfg_.rank != 0) {
+  if (!cfg_.isRoot()) {
     if (err) *err = "per-kernel counters need this rank's samples, which are gathered to rank 0";
     return Json();
   }
@@ -1426,7 +1432,7 @@ Json Agent::stats() const {
   j["gather_latency_us_avg"] = nt ? gatherLatSumNs_.load() / static_cast<double>(nt) * 1e-3 : 0.0;
   j["gather_latency_us_max"] = gatherLatMaxNs_.load() * 1e-3;
   j["gather_latency_us_last"] = gatherLatLastNs_.load() * 1e-3;
-  if (cfg_.rank == 0) j["drain_bytes"] = static_cast<unsigned long long>(drainBytes_.load());
+  if (cfg_.isRoot()) j["drain_bytes"] = static_cast<unsigned long long>(drainBytes_.load());
   if (shmMode_) j["shm_full_steps"] = static_cast<unsigned long long>(shmFull_.load());
   if (slotRing_) {
     j["slot_ring"] = cfg_.slotRing;
@@ -1466,7 +1472,7 @@ Json Agent::stats() const {
   }
   j["last_error"] = lastError_;
   if (sampler_) j["agent"] = sampler_->agent().name;
-  if (cfg_.rank == 0) {
+  if (cfg_.isRoot()) {
     std::lock_guard<std::mutex> lk(aggMu_);
     j["ranks"] = agg_.rankStats();
   }

@@ -56,10 +56,15 @@ struct AgentConfig {
   std::vector<int> rankLabels;
   int jobWorld = 0;        // ranks in the job (0: = world)
   int jobRank() const { return rankLabels.empty() ? rank : rankLabels.at(static_cast<size_t>(rank)); }
+  // receives and logs the group's samples
+  bool isRoot() const { return rank == 0 && !forceNonRoot; }
   double sampleHz = 1000.0;
   int batch = 32;                    // samples per H2D copy + pack launch
   int stages = 64;                   // pinned staging batches in flight (<= 256)
   bool forceCollective = false;      // testing: use the RCCL path (1-rank comm) at world 1
+  bool forceNonRoot = false;         // testing (with forceCollective at world 1): run this rank
+                                     // as a non-root gather member (no receive buffers, no
+                                     // consumer; the 1-rank gather runs in place)
   uint64_t ringSlots = 1ull << 20;   // 256 MiB of HBM history per GPU
   uint32_t gatherCapSlots = 4096;    // max slots per rank per gather (1 MiB); the
                                      // collective path agrees a smaller size each step

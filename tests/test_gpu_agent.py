@@ -614,3 +614,34 @@ def test_step_inside_graph_capture_is_skipped(native_built):
     assert res["steps_skipped_in_graph_capture"] == 1, res
     assert res["last_error"] == "" and res["samples_failed"] == 0, res
     assert res["ranks"][0]["received"] > 500, res
+
+
+def test_rccl_gather_path_as_non_root_member(native_built):
+    """The collective path of a gather MEMBER (rank > 0 in gather mode: no
+    receive buffers, no consumer thread, the payload agreement and the timed
+    gather on the trainer's stream), run on one GPU through a 1-rank
+    communicator in non-root role (the gather runs in place).  A missing
+    per-step event on exactly this path would have failed every rank > 0."""
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit()
+        import json, torch
+        torch.cuda.set_device(0)
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), gather_mode="gather",
+                                 force_collective=True, force_collective_role="nonroot")
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        for _ in range(40):
+            for _ in range(10):
+                y = x @ x
+            a.step()
+        torch.cuda.synchronize()
+        a.pack_pending(); a.step(); torch.cuda.synchronize()
+        st = a.stats(); a.stop()
+        print("RESULT " + json.dumps(st))
+    """)
+    st = res
+    assert st["collective"] is True and st["last_error"] == "" and not st["gather_failed"], st
+    assert st["gathers"] >= 40 and st["gather_slots"] > 200, st
+    assert st["gather_cap_slots_now"] < 4096, st          # the agreement sized the payload
+    assert st["gather_latency_samples"] >= 30, st
+    assert "drain_bytes" not in st and "ranks" not in st, st  # a member neither drains nor logs
