@@ -576,8 +576,20 @@ double threadCpuSec(clockid_t c) {
 }
 }  // namespace
 
+namespace {
+// The agent's threads sync on their own streams and events while the
+// trainer may be capturing a hipGraph in global mode, which prohibits such
+// calls in every thread that has not opted out: opt out (relaxed), so a
+// captured training step and the 1 kHz sampler coexist.
+void relaxGraphCaptureRules() {
+  hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&m);
+}
+}  // namespace
+
 void Agent::samplerLoop() {
   if (pthread_getcpuclockid(pthread_self(), &samplerClock_) == 0) samplerClockValid_ = true;
+  relaxGraphCaptureRules();
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
   uint64_t next = monoNs();
   int staged = 0;
@@ -920,6 +932,7 @@ bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err
 
 void Agent::consumerLoop() {
   if (pthread_getcpuclockid(pthread_self(), &consumerClock_) == 0) consumerClockValid_ = true;
+  relaxGraphCaptureRules();
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
   while (true) {
     int slot = -1;
@@ -1090,6 +1103,7 @@ void Agent::resume() { paused_ = false; }
 // Control channel to the node daemon: periodic "gctx" registration and
 // on-demand kernel traces ("gktr" -> KernelTracer -> "gktd").
 void Agent::controlLoop() {
+  relaxGraphCaptureRules();
   const int pid = static_cast<int>(getpid());
   uint64_t nextKeepalive = 0;
   while (!stopFlag_) {
