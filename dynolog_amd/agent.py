@@ -86,6 +86,20 @@ def _node_name(rank: int, world: int) -> str:
     return socket.gethostname()
 
 
+def default_gather_cap(sample_hz: float, gather_mode: str) -> int:
+    """Slots one rank may send per step: ~8 s of samples (a power of two,
+    4096..65536; free-running counts as 4 kHz) so steps of several seconds
+    lose nothing; the shm mailbox keeps 4096 (its blocks live in /dev/shm)."""
+    if gather_mode == "shm":
+        return 4096
+    hz = sample_hz if sample_hz > 0 else 4000.0
+    want = int(8 * hz)
+    cap = 4096
+    while cap < want and cap < 65536:
+        cap *= 2
+    return cap
+
+
 def plan_gather_group(rank: int, world: int, hosts: Sequence[str], scope: str = "node"):
     """The ranks one agent gather spans.
 
@@ -257,7 +271,7 @@ class GpuAgent:
     @classmethod
     def start(cls, device: int = 0, rank: int = 0, world: int = 1,
               sample_hz: float = 1000.0, batch: int = 32, ring_slots: int = 1 << 20,
-              gather_cap_slots: int = 4096, gather_mode: str = "gather", counter_set: str = "lite",
+              gather_cap_slots: Optional[int] = None, gather_mode: str = "gather", counter_set: str = "lite",
               log_interval_ms: int = 1000, sinks: Sequence[str] = ("json",),
               log_file: str = "", uid: Optional[bytes] = None, process_group=None,
               daemon_endpoint: str = "dynolog", fault_inject: str = "",
@@ -267,6 +281,11 @@ class GpuAgent:
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
+
+        ``gather_cap_slots``: most slots one rank sends per step (None: ~8 s of
+        samples at ``sample_hz`` for the RCCL modes, 4096 for the shm mailbox,
+        whose blocks live in /dev/shm); the RCCL payload itself is sized each
+        step from the ranks' pending slots, so the cap only bounds memory.
 
         ``gather_mode``: "gather" (ncclGather to rank 0 over xGMI, default),
         "allgather", "shm" (one node: ranks > 0 publish into a shared-memory
@@ -289,6 +308,7 @@ class GpuAgent:
         if not _preinit_done:
             raise AgentError("dynolog_amd.agent.preinit() must be called before HIP init")
         lib = _native.load_gpu_lib()
+        cap = gather_cap_slots or default_gather_cap(sample_hz, gather_mode)
         g_rank, g_world, labels = rank, world, None
         if world > 1 and gather_mode != "none" and uid is None:
             import torch.distributed as dist
@@ -311,7 +331,7 @@ class GpuAgent:
                 uid = ids[labels[0]]
         cfg = dict(device=device, rank=g_rank, world=g_world, sample_hz=sample_hz, batch=batch,
                    stages=stages,
-                   ring_slots=ring_slots, gather_cap_slots=gather_cap_slots,
+                   ring_slots=ring_slots, gather_cap_slots=cap,
                    gather_mode=gather_mode, counter_set=counter_set, log_interval_ms=log_interval_ms,
                    sinks=list(sinks), log_file=log_file, daemon_endpoint=daemon_endpoint)
         if counter_passes:

@@ -318,7 +318,7 @@ def test_rccl_gather_path_with_one_rank(native_built, mode):
         import json, time, torch
         torch.cuda.set_device(0)
         a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), gather_mode={mode!r},
-                                 force_collective=True)
+                                 force_collective=True, gather_cap_slots=4096)
         x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
         t0 = agent.mono_ns()
         for _ in range(40):
