@@ -229,3 +229,15 @@ def test_plan_gather_group_per_node():
     assert plan_gather_group(0, 1, ["a"]) == (0, 1, None)
     with pytest.raises(ValueError):
         plan_gather_group(0, 2, ["a", "a"], "rack")
+
+
+def test_default_gather_cap_covers_long_steps():
+    """The per-step payload cap holds ~8 s of samples (steps of several
+    seconds lose nothing); the shm mailbox keeps its /dev/shm-sized blocks."""
+    from dynolog_amd.agent import default_gather_cap
+    assert default_gather_cap(1000.0, "gather") == 8192
+    assert default_gather_cap(1000.0, "allgather") == 8192
+    assert default_gather_cap(1000.0, "shm") == 4096
+    assert default_gather_cap(100.0, "gather") == 4096        # floor
+    assert default_gather_cap(0.0, "gather") == 32768         # free-running ~4 kHz
+    assert default_gather_cap(50000.0, "gather") == 65536     # ceiling
