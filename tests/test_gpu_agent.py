@@ -616,18 +616,19 @@ def test_step_inside_graph_capture_is_skipped(native_built):
     assert res["ranks"][0]["received"] > 500, res
 
 
-def test_rccl_gather_path_as_non_root_member(native_built):
+@pytest.mark.parametrize("mode", ["gather", "allgather"])
+def test_rccl_gather_path_as_non_root_member(native_built, mode):
     """The collective path of a gather MEMBER (rank > 0 in gather mode: no
     receive buffers, no consumer thread, the payload agreement and the timed
     gather on the trainer's stream), run on one GPU through a 1-rank
     communicator in non-root role (the gather runs in place).  A missing
     per-step event on exactly this path would have failed every rank > 0."""
-    res = _run("""
+    res = _run(f"""
         from dynolog_amd import agent
         agent.preinit()
         import json, torch
         torch.cuda.set_device(0)
-        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), gather_mode="gather",
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), gather_mode={mode!r},
                                  force_collective=True, force_collective_role="nonroot")
         x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
         for _ in range(40):
