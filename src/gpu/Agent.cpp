@@ -1015,9 +1015,9 @@ void Agent::setPhaseName(uint32_t id, const std::string& name) {
   agg_.setPhaseName(id, name);
 }
 
-std::vector<Json> Agent::counterTrackEvents(uint64_t t0, uint64_t t1) const {
+std::vector<Json> Agent::counterTrackEvents(uint64_t t0, uint64_t t1, int device) const {
   std::lock_guard<std::mutex> lk(aggMu_);
-  return agg_.counterTrackEvents(t0, t1, static_cast<int>(getpid()));
+  return agg_.counterTrackEvents(t0, t1, static_cast<int>(getpid()), device);
 }
 
 void Agent::waitSamplesThrough(uint64_t t1) const {
@@ -1130,6 +1130,36 @@ void Agent::controlLoop() {
       res["pid"] = pid;
       res["rank"] = cfg_.jobRank();
       res["device"] = cfg_.device;
+      if (req.contains("op") && req.at("op").isString() && req.at("op").asString() == "counter_tracks") {
+        // the 1 kHz counter tracks of [t0_ns, t1_ns] (CLOCK_MONOTONIC), for a
+        // Kineto trace the daemon is annotating; only an aggregator holds them
+        if (!cfg_.isRoot()) {
+          res["status"] = "not an aggregator";
+        } else {
+          const uint64_t t0 = static_cast<uint64_t>(req.at("t0_ns").asInt());
+          const uint64_t t1 = static_cast<uint64_t>(req.at("t1_ns").asInt());
+          const int dev = req.contains("device") ? static_cast<int>(req.at("device").asInt()) : -1;
+          if (!paused_) packPending();
+          waitSamplesThrough(std::min<uint64_t>(t1, monoNs()));
+          Json ev = Json::array();
+          for (auto& e : counterTrackEvents(t0, t1, dev)) ev.push_back(std::move(e));
+          res["num_events"] = static_cast<unsigned long long>(ev.size());
+          // thousands of events do not fit a datagram: written to the file the
+          // daemon names (next to the trace, writable by this process)
+          const std::string path = req.contains("out_path") ? req.at("out_path").asString() : "";
+          std::ofstream f(path);
+          if (path.empty() || !f) {
+            res["status"] = "failed: cannot write '" + path + "'";
+          } else {
+            f << ev.dump();
+            f.close();
+            res["status"] = f ? "ok" : "failed: write error on '" + path + "'";
+            res["events_path"] = path;
+          }
+        }
+        (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, res.dump()), msg->src, 3, 10000);
+        continue;
+      }
       auto& kt = KernelTracer::get();
       const int dur = req.contains("duration_ms") ? static_cast<int>(req.at("duration_ms").asInt()) : 500;
       const int top = req.contains("top") ? static_cast<int>(req.at("top").asInt()) : 20;

@@ -112,7 +112,7 @@ class Agent {
   Json phaseStats() const;
   // Counter-track trace events of the samples in [t0, t1] (rank 0 sees every
   // rank's; other ranks have none) for KernelTracer::writeChromeTrace.
-  std::vector<Json> counterTrackEvents(uint64_t t0, uint64_t t1) const;
+  std::vector<Json> counterTrackEvents(uint64_t t0, uint64_t t1, int device = -1) const;
   // Kernel trace Chrome JSON with this agent's counter tracks under it.
   bool writeKernelTrace(const std::string& path, std::string* err) const;
   // Per-kernel counters of the last kernel-trace window: this process's

@@ -287,9 +287,10 @@ std::vector<uint64_t> SlotAggregator::windowCounts(uint64_t t0, uint64_t t1) con
   return out;
 }
 
-std::vector<Json> SlotAggregator::counterTrackEvents(uint64_t t0, uint64_t t1, int pid) const {
+std::vector<Json> SlotAggregator::counterTrackEvents(uint64_t t0, uint64_t t1, int pid, int device) const {
   std::vector<Json> out;
   for (int r = 0; r < world(); ++r) {
+    if (device >= 0 && ranks_[static_cast<size_t>(r)].device != device) continue;
     const auto& h = ranks_[static_cast<size_t>(r)].hist;
     auto lo = std::lower_bound(h.begin(), h.end(), t0,
                                [](const TraceSample& x, uint64_t t) { return x.ts < t; });

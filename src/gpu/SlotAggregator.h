@@ -129,7 +129,8 @@ class SlotAggregator {
   // [t0, t1] (CLOCK_MONOTONIC ns): one track per rank and metric group
   // (MFMA util %, bf16 TFLOP/s, HBM GB/s read/write, GPU busy %, sclk), so
   // a kernel timeline shows the 1 kHz counters under its dispatches.
-  std::vector<Json> counterTrackEvents(uint64_t t0, uint64_t t1, int pid) const;
+  // device >= 0: only the ranks whose gather headers name that GPU
+  std::vector<Json> counterTrackEvents(uint64_t t0, uint64_t t1, int pid, int device = -1) const;
   // samples kept per rank for counterTrackEvents (default 2^17, ~2 min at 1 kHz)
   void setHistoryCap(size_t n) { histCap_ = std::max<size_t>(n, 1); }
   const RankAggregate& rank(int r) const { return ranks_.at(static_cast<size_t>(r)); }

@@ -105,7 +105,13 @@ std::shared_ptr<RpcDispatcher> makeDispatcher(std::shared_ptr<ServiceHandler> h)
         if (!l.isNumber()) l.asDouble();  // throws
         limit = static_cast<int32_t>(l.asInt());
       }
-      return h->setKinetOnDemandRequest(jobId, pids, config, limit).toJson();
+      const auto res = h->setKinetOnDemandRequest(jobId, pids, config, limit);
+      Json reply = res.toJson();
+      // dynolog-amd extension; without the field the reply is the reference's
+      if (req.contains("gpu_counters") && req.at("gpu_counters").isBool() && req.at("gpu_counters").asBool() &&
+          h->gpuTraceHook())
+        h->gpuTraceHook()(req, res, &reply);
+      return reply;
     } catch (const std::exception& e) {
       LOG(ERROR) << "setKinetOnDemandRequest: parsing exception = " << e.what();
       r["status"] = std::string("failed with exception = ") + e.what();

@@ -6,6 +6,8 @@
 // through a template parameter, tests/rpc/SimpleJsonClientTest.cpp:21-50).
 #pragma once
 
+#include <functional>
+
 #include <memory>
 #include <set>
 #include <string>
@@ -37,11 +39,18 @@ class ServiceHandler {
   void setMetricStore(std::shared_ptr<MetricStore> s) { store_ = std::move(s); }
   const std::shared_ptr<MetricStore>& store() const { return store_; }
   void setConfigManager(tracing::KinetoConfigManager* m) { mgr_ = m; }
+  // Extension of setKinetOnDemandRequest: a request carrying
+  // "gpu_counters": true is handed here with its reply (the daemon starts a
+  // job that adds the GPU agents' counter tracks to the traces once written).
+  using GpuTraceHook = std::function<void(const Json& req, const tracing::GpuProfilerResult& res, Json* reply)>;
+  void setGpuTraceHook(GpuTraceHook h) { gpuTraceHook_ = std::move(h); }
+  const GpuTraceHook& gpuTraceHook() const { return gpuTraceHook_; }
 
  protected:
   tracing::KinetoConfigManager& mgr();
   std::shared_ptr<MetricStore> store_;
   tracing::KinetoConfigManager* mgr_ = nullptr;
+  GpuTraceHook gpuTraceHook_;
 };
 
 std::shared_ptr<RpcDispatcher> makeDispatcher(std::shared_ptr<ServiceHandler> handler);

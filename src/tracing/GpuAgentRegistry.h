@@ -45,6 +45,12 @@ class GpuAgentRegistry {
   // their summaries (waits up to durationMs + slackMs).
   Json kernelTrace(const std::vector<int>& pids, int durationMs, int top, const std::string& chromeDir,
                    const Sender& send, int slackMs = 10000);
+  // Ask every live agent for its 1 kHz counter tracks of [t0Ns, t1Ns]
+  // (CLOCK_MONOTONIC) of GPU `device` (-1: all); aggregators write them to
+  // "<pathPrefix><pid>.json".  Returns the events of every agent that had
+  // some (the files are read and removed).
+  std::vector<Json> counterTracks(uint64_t t0Ns, uint64_t t1Ns, int device, const std::string& pathPrefix,
+                                  const Sender& send, int timeoutMs = 5000);
 
  private:
   void gcLocked(uint64_t now);

@@ -16,8 +16,8 @@ from dynolog_amd.utils.daemon import DaemonProcess
 pytestmark = pytest.mark.slow
 
 
-@pytest.mark.parametrize("switches", [(), ("--record-shapes", "--with-stacks")],
-                         ids=["default", "shapes+stacks"])
+@pytest.mark.parametrize("switches", [(), ("--record-shapes", "--with-stacks"), ("--gpu-counters",)],
+                         ids=["default", "shapes+stacks", "gpu-counters"])
 def test_libkineto_registers_and_traces(native_built, tmp_path, switches):
     # Filesystem-socket mode keeps the test isolated from any system daemon.
     # sun_path is 108 bytes and libkineto's client name carries a 36-char
@@ -30,6 +30,15 @@ def test_libkineto_registers_and_traces(native_built, tmp_path, switches):
     finally:
         shutil.rmtree(sockdir, ignore_errors=True)
     ops = [e for e in trace["traceEvents"] if e.get("cat") == "cpu_op"]
+    if "--gpu-counters" in switches:
+        # the daemon's job waited for the trace file and found no GPU agent to
+        # ask (CPU host): the trace is left as libkineto wrote it
+        job = trace["_gpu_counters_job"]
+        assert job["status"] == "no counter tracks added", job
+        assert job["files"][0]["path"].endswith(".json"), job
+        assert "no counter samples" in job["files"][0]["status"], job
+        assert "dynologGpuCounters" not in trace
+        return
     if "--record-shapes" in switches:
         # the optional content really reaches the real libkineto/profiler:
         # aten::mm carries its input shapes only when the switch is on
@@ -92,6 +101,18 @@ def _run(native_built, tmp_path, sockdir, switches=()):
             with open(out) as f:
                 trace = json.load(f)
             assert "traceEvents" in trace and len(trace["traceEvents"]) > 0
+            if "--gpu-counters" in switches:
+                import re
+                m = re.search(r"daemon job (\d+)", r.stdout)
+                assert m, r.stdout
+                deadline = time.time() + 60
+                res = {}
+                while time.time() < deadline:
+                    res = d.rpc({"fn": "getTraceResult", "job_id": int(m.group(1))})
+                    if res.get("status") != "running":
+                        break
+                    time.sleep(0.25)
+                trace["_gpu_counters_job"] = res
             return trace
         finally:
             done.write_text("1")
