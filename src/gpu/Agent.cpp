@@ -208,6 +208,9 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     log::setSink([f](log::Severity, const std::string& l) { *f << l << "\n" << std::flush; });
   }
   HIP_OK(hipSetDevice(cfg_.device), "hipSetDevice");
+  // make sure the runtime (and with it HSA, which the counting contexts
+  // need) is up: a trainer may start the agent before its first GPU call
+  HIP_OK(hipFree(nullptr), "HIP runtime init");
   // leftovers of an earlier start() that failed part-way (the caller may
   // retry with another gather mode, agent.py)
   if (sampler_) sampler_->stop();
