@@ -241,3 +241,19 @@ def test_default_gather_cap_covers_long_steps():
     assert default_gather_cap(100.0, "gather") == 4096        # floor
     assert default_gather_cap(0.0, "gather") == 32768         # free-running ~4 kHz
     assert default_gather_cap(50000.0, "gather") == 65536     # ceiling
+
+
+def test_loading_the_agent_library_does_not_import_torch(native_built):
+    """The agent library binds to torch's ROCm runtime by preloading torch's
+    libraries, not by importing torch: with KINETO_USE_DAEMON set, `import
+    torch` brings up libkineto's roctracer and the HIP runtime, after which
+    the rocprofiler-sdk tool could no longer be registered (profiles/round3/g15)."""
+    import subprocess
+    import sys
+    code = ("import sys; from dynolog_amd import _native; lib = _native.load_gpu_lib(); "
+            "print('torch' in sys.modules, len(_native.preload_torch_runtime()) > 0)")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=repo, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=repo, KINETO_USE_DAEMON="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split() == ["False", "True"], r.stdout
