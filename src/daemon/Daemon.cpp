@@ -231,7 +231,9 @@ bool Daemon::start(std::string* err) {
         auto fetch = [&](uint64_t t0, uint64_t t1, int dev) {
           return gpuAgents_->counterTracks(t0, t1, dev, path + ".gpuctr_", send);
         };
-        Json r = tracing::annotateKinetoTrace(path, trace, fetch, tracing::monoToWallOffsetNs());
+        int dev = -1;  // the traced process's GPU, from its agent's registration
+        for (const auto& a : gpuAgents_->agents({pid})) dev = a.device;
+        Json r = tracing::annotateKinetoTrace(path, trace, fetch, tracing::monoToWallOffsetNs(), dev);
         added += r.contains("events_added") ? static_cast<size_t>(r.at("events_added").asInt()) : 0;
         files.push_back(r);
       }

@@ -146,7 +146,7 @@ bool waitForTraceFile(const std::string& path, int timeoutMs, Json* out, std::st
 }
 
 Json annotateKinetoTrace(const std::string& path, const Json& traceIn, const CounterFetch& fetch,
-                         int64_t monoToWallNs) {
+                         int64_t monoToWallNs, int agentDevice) {
   Json res = Json::object();
   res["path"] = path;
   KinetoWindow w;
@@ -165,15 +165,23 @@ Json annotateKinetoTrace(const std::string& path, const Json& traceIn, const Cou
   auto& evs = trace["traceEvents"].asArray();
   size_t added = 0;
   Json devs = Json::array();
-  std::vector<int64_t> lanes(w.gpuPids.begin(), w.gpuPids.end());
-  if (lanes.empty()) lanes.push_back(-1);  // no GPU activity recorded: all of the agent's GPUs
-  for (int64_t dev : lanes) {
-    auto got = fetch(m0, m1, static_cast<int>(dev));
-    rebaseCounterEvents(got, monoToWallNs, w.baseNs, dev >= 0 ? dev : 0);
+  // (lane in the trace, device to ask the agents for)
+  std::vector<std::pair<int64_t, int>> lanes;
+  if (w.gpuPids.size() == 1) {
+    lanes.emplace_back(*w.gpuPids.begin(), agentDevice);
+  } else if (w.gpuPids.empty()) {
+    lanes.emplace_back(agentDevice >= 0 ? agentDevice : 0, agentDevice);  // no GPU activity recorded
+  } else {
+    for (int64_t p : w.gpuPids) lanes.emplace_back(p, static_cast<int>(p));
+  }
+  for (const auto& [lane, dev] : lanes) {
+    auto got = fetch(m0, m1, dev);
+    rebaseCounterEvents(got, monoToWallNs, w.baseNs, lane);
     for (auto& e : got) evs.push_back(std::move(e));
     added += got.size();
     Json d = Json::object();
-    d["device"] = static_cast<long long>(dev);
+    d["lane"] = static_cast<long long>(lane);
+    d["device"] = dev;
     d["events"] = static_cast<unsigned long long>(got.size());
     devs.push_back(d);
   }

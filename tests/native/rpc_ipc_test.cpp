@@ -511,7 +511,7 @@ TEST(TraceAnnotator, CounterTracksJoinTheKinetoTimeline) {
   Json r = annotateKinetoTrace(path, loaded, fetch, off);
   EXPECT_EQ(r.at("status").asString(), std::string("ok"));
   EXPECT_EQ(r.at("events_added").asInt(), 3);
-  EXPECT_EQ(askedDev, 3);
+  EXPECT_EQ(askedDev, -1);  // one GPU lane, agent device unknown: all of the agent's GPUs
   // the GPU window in monotonic ns: base + ts*1000 - off
   EXPECT_EQ(askedT0, static_cast<uint64_t>(base - off + 1000000));
   EXPECT_EQ(askedT1, static_cast<uint64_t>(base - off + 3000000));
