@@ -642,7 +642,7 @@ def test_rccl_gather_path_as_non_root_member(native_built, mode):
     """)
     st = res
     assert st["collective"] is True and st["last_error"] == "" and not st["gather_failed"], st
-    assert st["gathers"] >= 40 and st["gather_slots"] > 200, st
+    assert st["gathers"] >= 40 and st["gather_slots"] > 100, st
     assert st["gather_cap_slots_now"] < 4096, st          # the agreement sized the payload
     assert st["gather_latency_samples"] >= 30, st
     assert "drain_bytes" not in st and "ranks" not in st, st  # a member neither drains nor logs
