@@ -23,6 +23,7 @@ BUILD_DIR = os.path.join(REPO_ROOT, "build")
 LIB_DIR = os.path.join(REPO_ROOT, "dynolog_amd", "lib")
 GPU_LIB = os.path.join(LIB_DIR, "libdyno_gpu.so")
 ROCPROF_LIB = os.path.join(LIB_DIR, "libdyno_rocprof.so")  # rocprofiler-sdk tool half (no HIP dependency)
+RPTOOL_LIB = os.path.join(LIB_DIR, "libdyno_rptool.so")   # its tool-discovery shim (ROCP_TOOL_LIBRARIES)
 OPS_LIB = os.path.join(LIB_DIR, "libdyno_ops.so")
 
 _build_lock = threading.Lock()
