@@ -382,7 +382,9 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   // has no receive buffer but orders its agreement copy after the gather)
   for (int i = 0; i < kRecv; ++i) {
     HIP_OK(hipEventCreateWithFlags(&gathered_[i], hipEventDisableTiming), "event");
-    HIP_OK(hipEventCreateWithFlags(&drained_[i], hipEventDisableTiming), "event");
+    // the consumer thread waits on this one for up to a training step (the
+    // drain copy is ordered after the step's gather): sleep, do not spin
+    HIP_OK(hipEventCreateWithFlags(&drained_[i], hipEventDisableTiming | hipEventBlockingSync), "event");
     recvUsed_[i] = false;
   }
   if (collective_) {
