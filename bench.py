@@ -436,6 +436,8 @@ def main(argv=None) -> int:
                 if base_s:
                     # the price of the registered-but-paused agent itself
                     out["paused_vs_no_agent_pct"] = round((base_s / args.steps * 1e3 / no_agent_ms - 1.0) * 100.0, 3)
+        if torch.distributed.is_initialized():
+            out["dist_backend"] = torch.distributed.get_backend()
         if ag is not None:
             # ranks per gather group (= n_gpus on one node; one group per node otherwise)
             out["gather_group_size"] = ag.gather_world
