@@ -384,7 +384,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     HIP_OK(hipEventCreateWithFlags(&gathered_[i], hipEventDisableTiming), "event");
     // the consumer thread waits on this one for up to a training step (the
     // drain copy is ordered after the step's gather): sleep, do not spin
-    HIP_OK(hipEventCreateWithFlags(&drained_[i], hipEventDisableTiming | hipEventBlockingSync), "event");
+    HIP_OK(hipEventCreateWithFlags(&drained_[i], hipEventDisableTiming), "event");
     recvUsed_[i] = false;
   }
   if (collective_) {
@@ -953,7 +953,15 @@ void Agent::consumerLoop() {
       }
     }
     if (slot >= 0) {
-      const bool ok = hipWarn(hipEventSynchronize(drained_[slot]), "drain wait");
+      // The drain completes only after the step's GPU work (it is ordered
+      // behind the gather on the trainer's stream), i.e. up to a whole step
+      // later.  The runtime's wait spun for that long even on a blocking-sync
+      // event (54 % of a core, g19 / g21), so poll at 1 ms: the records are
+      // logged once a second and a late ingest costs nothing.
+      hipError_t q;
+      while ((q = hipEventQuery(drained_[slot])) == hipErrorNotReady)
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      const bool ok = hipWarn(q, "drain wait");
       std::lock_guard<std::mutex> lk(aggMu_);
       auto onSlot = [this](const DynoSlot& s) {
         if (slotProd_ && slotProd_->write(s) < 0) {
