@@ -187,6 +187,7 @@ class Agent {
   hipEvent_t gathered_[kRecv] = {};
   hipEvent_t drained_[kRecv] = {};
   bool recvUsed_[kRecv] = {};
+  bool recvPending_[kRecv] = {};        // drained buffer not yet ingested by the consumer (aggMu_)
   int recvNext_ = 0;
 
   // host staging (pinned): cfg_.stages batches may be in flight (H2D copy +
@@ -234,7 +235,7 @@ class Agent {
   hipEvent_t agreeDone_[kAgree] = {};
   uint64_t collectiveGathers_ = 0;  // gathers issued through RCCL (stepMu_)
   uint32_t recvCap_[kRecv] = {};        // payload cap of the gather in each recv buffer
-  std::atomic<uint64_t> gatherBytes_{0}, gatherSlots_{0}, drainBytes_{0}, runAheadWaits_{0};
+  std::atomic<uint64_t> gatherBytes_{0}, gatherSlots_{0}, drainBytes_{0}, runAheadWaits_{0}, recvWaits_{0};
   std::atomic<uint64_t> backlogNow_{0}, capNow_{0};
   std::atomic<uint64_t> captureSkips_{0};  // step() calls inside a hipGraph capture
   bool gatherCollective(hipStream_t stream, uint64_t head, std::string* err);
@@ -253,6 +254,7 @@ class Agent {
   int beginGatherTimer(hipStream_t stream);  // -1: no free timer (stepMu_)
   void endGatherTimer(int idx, hipStream_t stream);
   void harvestGatherTimers();
+  void waitRecvIngested(int slot);
   std::atomic<uint64_t> gatherTimed_{0}, gatherLatSumNs_{0}, gatherLatMaxNs_{0}, gatherLatLastNs_{0};
 
   ncclComm_t comm_ = nullptr;
