@@ -111,8 +111,8 @@ Agent* Agent::instance() {
   return a;
 }
 
-bool Agent::preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace) {
-  return RocprofRuntime::get().preinit(agentIndices, err, kernelTrace);
+bool Agent::preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace, bool threadTrace) {
+  return RocprofRuntime::get().preinit(agentIndices, err, kernelTrace, threadTrace);
 }
 
 namespace {

@@ -91,7 +91,8 @@ struct AgentConfig {
 class Agent {
  public:
   static Agent* instance();
-  static bool preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace = false);
+  static bool preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace = false,
+                      bool threadTrace = false);
 
   bool start(const AgentConfig& cfg, const void* ncclUniqueId, size_t idLen, std::string* err);
   // Enqueue the rank-0 gather on `stream` (nullptr = legacy default stream).
@@ -121,6 +122,7 @@ class Agent {
   Json kernelCounters(size_t top, std::string* err) const;
   void stop();
   bool running() const { return running_; }
+  bool paused() const { return paused_; }
 
   Json stats() const;
   // Slots per rank whose sample time lies in [t0, t1] (CLOCK_MONOTONIC ns).

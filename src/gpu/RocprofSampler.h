@@ -55,7 +55,9 @@ class RocprofRuntime {
   // (with reason) if the runtime is already locked or rocprofiler fails.
   // kernelTrace: also configure on-demand kernel dispatch tracing
   // (KernelTracer.h; makes rocprofiler intercept the HSA queues).
-  bool preinit(const std::vector<int>& devices, std::string* err, bool kernelTrace = false);
+  // threadTrace: also configure on-demand SQTT capture (ThreadTracer)
+  bool preinit(const std::vector<int>& devices, std::string* err, bool kernelTrace = false,
+               bool threadTrace = false);
   // Discovery path (ROCP_TOOL_LIBRARIES, set by the Python preinit() when
   // importing torch would initialise HIP first): rocprofiler-sdk loads this
   // library at HSA init and calls the exported rocprofiler_configure, which
@@ -84,6 +86,7 @@ class RocprofRuntime {
   bool toolInitDone_ = false;
   std::vector<int> wantDevices_;
   bool kernelTrace_ = false;
+  bool threadTrace_ = false;
   std::vector<AgentInfo> agents_;
   std::map<int, std::unique_ptr<Ctx>> ctxs_;
   std::string err_;

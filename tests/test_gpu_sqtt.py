@@ -1,0 +1,82 @@
+"""On-demand SQTT capture (src/gpu/ThreadTracer.h) on a real MI355X: the
+GPU counterpart of the reference's Intel PT AUX capture
+(hbt/src/perf_event/PerCpuTraceAuxGenerator.h).  Each scenario runs in its
+own process (the rocprofiler tool registers before HIP initialises)."""
+import json
+import os
+
+import pytest
+
+from test_gpu_agent import _run
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sqtt_captures_matching_gemm_dispatches(native_built, tmp_path):
+    out = str(tmp_path / "sqtt")
+    res = _run(f"""
+        from dynolog_amd import agent
+        agent.preinit(thread_trace=True)
+        import json, torch
+        torch.cuda.set_device(0)
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        y = x @ x; torch.cuda.synchronize()          # kernels loaded, names known
+        assert agent.ThreadTrace.configured()
+        tt = agent.ThreadTrace({out!r}, kernel_regex="Cijk|gemm|GEMM|matmul", dispatches=2).start()
+        for _ in range(4):
+            y = x @ x
+        torch.cuda.synchronize()
+        idx = tt.finish(timeout_s=20)
+        z = (x @ x).float().sum().item()             # untraced work still runs afterwards
+        print("RESULT " + json.dumps(dict(idx=idx, z=z)))
+    """, timeout=300)
+    idx = res["idx"]
+    print(json.dumps({k: v for k, v in idx.items() if k != "code_objects"}, indent=1)[:4000])
+    assert "error" not in idx, idx
+    assert idx["traced"] == 2 and idx["requested"] == 2, idx
+    for d in idx["dispatches"]:
+        assert d["kernel"], d
+        assert d["shader_engines"], d
+        for se in d["shader_engines"]:
+            assert se["bytes"] > 0 and os.path.getsize(os.path.join(out, se["file"])) == se["bytes"], se
+    assert idx["total_bytes"] > 0
+    # the traced kernels' code objects are named (file URI) or copied out
+    assert idx["code_objects"] and all(co["uri"] for co in idx["code_objects"]), idx["code_objects"]
+    assert os.path.exists(idx["index_path"])
+    assert res["z"] == res["z"]
+
+
+def test_sqtt_pauses_and_resumes_the_sampler(native_built, tmp_path):
+    """With the counter agent sampling, a capture of one of our own CDNA4
+    kernels pauses the sampler for the capture and resumes it afterwards; a
+    regex nothing matches returns an empty index with an error."""
+    out = str(tmp_path / "sqtt")
+    res = _run(f"""
+        from dynolog_amd import agent
+        agent.preinit(thread_trace=True)
+        import json, time, torch
+        torch.cuda.set_device(0)
+        from dynolog_amd import ops
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
+        x = torch.randn(8192, 4096, device="cuda", dtype=torch.bfloat16)
+        w = torch.ones(4096, device="cuda", dtype=torch.bfloat16)
+        y = ops.rms_norm(x, w, 1e-5); torch.cuda.synchronize()
+        time.sleep(0.2)
+        n0 = a.stats()["samples_taken"]
+        tt = agent.ThreadTrace({out!r}, kernel_regex="rms", dispatches=1).start()
+        for _ in range(3):
+            y = ops.rms_norm(x, w, 1e-5)
+        torch.cuda.synchronize()
+        idx = tt.finish(timeout_s=20)
+        none = agent.ThreadTrace({out!r}, kernel_regex="no_such_kernel_xyz", dispatches=1).start().finish(timeout_s=1)
+        time.sleep(0.3)
+        st = a.stats()
+        a.stop()
+        print("RESULT " + json.dumps(dict(idx=idx, none=none, n0=n0, st=st)))
+    """, timeout=300)
+    idx, none, st = res["idx"], res["none"], res["st"]
+    assert idx["traced"] == 1 and "rms" in idx["dispatches"][0]["kernel"].lower(), idx
+    assert idx["dispatches"][0]["shader_engines"][0]["bytes"] > 0, idx
+    assert none["traced"] == 0 and "no matching dispatch" in none.get("error", ""), none
+    # sampling resumed after the captures
+    assert st["samples_taken"] > res["n0"] + 100 and st["samples_failed"] == 0, st
