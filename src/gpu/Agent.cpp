@@ -14,6 +14,7 @@
 #include "common/Sync.h"
 #include "gpu/KernelCounters.h"
 #include "gpu/KernelTracer.h"
+#include "gpu/ThreadTracer.h"
 #include "gpu/ShmGather.h"
 #include "ipc/Fabric.h"
 #include "sinks/Prometheus.h"
@@ -1147,6 +1148,7 @@ void Agent::controlLoop() {
       c["device"] = cfg_.device;
       c["endpoint"] = ctl_->endpoint().name();
       c["kernel_trace"] = KernelTracer::get().configured();
+      c["thread_trace"] = ThreadTracer::get().configured();
       (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgAgentContext, c.dump()), cfg_.daemonEndpoint, 1, 0);
       nextKeepalive = now + 10'000'000'000ull;
     }
@@ -1192,6 +1194,11 @@ void Agent::controlLoop() {
         (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, res.dump()), msg->src, 3, 10000);
         continue;
       }
+      if (req.contains("op") && req.at("op").isString() && req.at("op").asString() == "sqtt") {
+        (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, sqttRequest(req, res).dump()),
+                             msg->src, 3, 10000);
+        continue;
+      }
       auto& kt = KernelTracer::get();
       const int dur = req.contains("duration_ms") ? static_cast<int>(req.at("duration_ms").asInt()) : 500;
       const int top = req.contains("top") ? static_cast<int>(req.at("top").asInt()) : 20;
@@ -1223,6 +1230,50 @@ void Agent::controlLoop() {
       (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, res.dump()), msg->src, 3, 10000);
     }
   }
+}
+
+// "sqtt" over the control channel: capture the next N matching dispatches
+// of this process (ThreadTracer), with the counter sampler paused, and
+// answer with a compact summary (the full index stays in its file: a
+// datagram cannot carry long symbol lists).
+Json Agent::sqttRequest(const Json& req, Json res) {
+  auto& tt = ThreadTracer::get();
+  SqttRequest r;
+  r.kernelRegex = req.contains("kernel_regex") && req.at("kernel_regex").isString() ? req.at("kernel_regex").asString() : "";
+  r.dispatches = req.contains("dispatches") ? static_cast<int>(req.at("dispatches").asInt()) : 1;
+  r.outDir = req.contains("out_dir") && req.at("out_dir").isString() ? req.at("out_dir").asString() : "";
+  r.agentIndex = sampler_ ? sampler_->agent().index : -1;
+  const int timeoutMs = req.contains("timeout_ms") ? static_cast<int>(req.at("timeout_ms").asInt()) : 10000;
+  const bool pauseHere = !paused_;
+  if (pauseHere) {
+    pause();
+    usleep(5000);  // the sampler loop stops its counting context within ~2 ms
+  }
+  std::string err;
+  if (!tt.start(r, &err)) {
+    res["status"] = "failed: " + err;
+  } else {
+    Json idx = tt.finish(timeoutMs, &err);
+    res["status"] = err.empty() ? "ok" : "failed: " + err;
+    for (const char* k : {"traced", "requested", "total_bytes", "index_path", "window_ms", "params"})
+      if (idx.contains(k)) res[k] = idx.at(k);
+    Json d = Json::array();
+    if (idx.contains("dispatches"))
+      for (const auto& x : idx.at("dispatches").asArray()) {
+        Json o = Json::object();
+        o["dispatch_id"] = x.at("dispatch_id");
+        std::string k = x.contains("kernel") ? x.at("kernel").asString() : "";
+        if (k.size() > 160) k = k.substr(0, 157) + "...";
+        o["kernel"] = k;
+        unsigned long long bytes = 0;
+        for (const auto& se : x.at("shader_engines").asArray()) bytes += static_cast<unsigned long long>(se.at("bytes").asInt());
+        o["bytes"] = bytes;
+        d.push_back(o);
+      }
+    res["dispatches"] = d;
+  }
+  if (pauseHere) resume();
+  return res;
 }
 
 Json Agent::kernelCounters(size_t top, std::string* err) const {

@@ -134,6 +134,7 @@ class Agent {
  private:
   void samplerLoop();
   void controlLoop();
+  Json sqttRequest(const Json& req, Json res);
   bool flushBatch(int nstaged, std::string* err);
   void consumerLoop();
   void logInterval();

@@ -27,6 +27,7 @@ void GpuAgentRegistry::onContext(const Json& j, const std::string& src) {
   e.device = static_cast<int>(getI(j, "device"));
   e.endpoint = j.contains("endpoint") && j.at("endpoint").isString() ? j.at("endpoint").asString() : src;
   e.kernelTrace = j.contains("kernel_trace") && j.at("kernel_trace").isBool() && j.at("kernel_trace").asBool();
+  e.threadTrace = j.contains("thread_trace") && j.at("thread_trace").isBool() && j.at("thread_trace").asBool();
   e.lastSeenNs = nowNsMonotonic();
   if (e.pid <= 0) return;
   std::lock_guard<std::mutex> g(mu_);
@@ -75,6 +76,7 @@ Json GpuAgentRegistry::listJson() {
     o["device"] = e.device;
     o["endpoint"] = e.endpoint;
     o["kernel_trace"] = e.kernelTrace;
+    o["thread_trace"] = e.threadTrace;
     o["last_seen_s"] = (now - e.lastSeenNs) * 1e-9;
     arr.push_back(o);
   }
@@ -116,6 +118,55 @@ Json GpuAgentRegistry::kernelTrace(const std::vector<int>& pids, int durationMs,
     std::unique_lock<std::mutex> lk(mu_);
     condWaitFor(cv_, lk, std::chrono::milliseconds(durationMs + slackMs),
                  [&] { return results_[id].size() >= expected; });
+    got = std::move(results_[id]);
+    results_.erase(id);
+  }
+  Json res = Json::array();
+  for (auto& r : got) res.push_back(r);
+  out["status"] = got.size() == expected ? "ok" : "partial";
+  out["requested"] = sent;
+  out["results"] = res;
+  return out;
+}
+
+Json GpuAgentRegistry::threadTrace(const std::vector<int>& pids, const std::string& kernelRegex, int dispatches,
+                                   const std::string& outDir, int timeoutMs, const Sender& send, int slackMs) {
+  Json out = Json::object();
+  std::vector<GpuAgentEntry> targets;
+  for (const auto& a : agents(pids))
+    if (a.threadTrace) targets.push_back(a);
+  if (targets.empty()) {
+    out["status"] = "failed: no GPU agent with thread trace registered" +
+                    std::string(pids.empty() ? "" : " for these pids") +
+                    " (the process must call agent.preinit(thread_trace=True))";
+    return out;
+  }
+  uint64_t id;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    id = nextId_++;
+    results_[id] = {};
+  }
+  Json sent = Json::array();
+  size_t expected = 0;
+  for (const auto& a : targets) {
+    Json req = Json::object();
+    req["id"] = static_cast<unsigned long long>(id);
+    req["op"] = "sqtt";
+    req["kernel_regex"] = kernelRegex;
+    req["dispatches"] = dispatches;
+    req["timeout_ms"] = timeoutMs;
+    req["out_dir"] = outDir + "/pid" + std::to_string(a.pid) + "_r" + std::to_string(a.rank);
+    if (send("gktr", req.dump(), a.endpoint)) {
+      ++expected;
+      sent.push_back(a.pid);
+    }
+  }
+  std::vector<Json> got;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    condWaitFor(cv_, lk, std::chrono::milliseconds(timeoutMs + slackMs),
+                [&] { return results_[id].size() >= expected; });
     got = std::move(results_[id]);
     results_.erase(id);
   }

@@ -4,6 +4,8 @@
 //   agent  -> daemon  "gctx" {pid, rank, device, endpoint, kernel_trace}   (register / keepalive)
 //   daemon -> agent   "gktr" {id, duration_ms, top, chrome_path}           (trace request)
 //   agent  -> daemon  "gktd" {id, pid, rank, status, summary}              (result)
+//   daemon -> agent   "gktr" {id, op:"sqtt", kernel_regex, dispatches, out_dir, timeout_ms}
+//                                                    (SQTT capture, answered with "gktd")
 //
 // The registry plays the role LibkinetoConfigManager plays for libkineto
 // processes (reference LibkinetoConfigManager.cpp:146-191: registration on
@@ -27,6 +29,7 @@ struct GpuAgentEntry {
   int pid = 0, rank = 0, device = 0;
   std::string endpoint;
   bool kernelTrace = false;
+  bool threadTrace = false;
   uint64_t lastSeenNs = 0;
 };
 
@@ -45,6 +48,11 @@ class GpuAgentRegistry {
   // their summaries (waits up to durationMs + slackMs).
   Json kernelTrace(const std::vector<int>& pids, int durationMs, int top, const std::string& chromeDir,
                    const Sender& send, int slackMs = 10000);
+  // Ask every matching agent to capture SQTT of its next `dispatches`
+  // kernels matching `kernelRegex` into "<outDir>/pid<pid>_r<rank>" and
+  // collect their summaries (waits up to timeoutMs + slackMs).
+  Json threadTrace(const std::vector<int>& pids, const std::string& kernelRegex, int dispatches,
+                   const std::string& outDir, int timeoutMs, const Sender& send, int slackMs = 5000);
   // Ask every live agent for its 1 kHz counter tracks of [t0Ns, t1Ns]
   // (CLOCK_MONOTONIC) of GPU `device` (-1: all); aggregators write them to
   // "<pathPrefix><pid>.json".  Returns the events of every agent that had
