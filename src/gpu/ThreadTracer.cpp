@@ -161,11 +161,7 @@ bool ThreadTracer::configure(const std::vector<std::pair<uint64_t, int>>& agents
   return configured_;
 }
 
-bool ThreadTracer::start(const SqttRequest& req, std::string* err) {
-  if (!configured_) {
-    if (err) *err = "thread trace not configured (preinit with thread_trace enabled)";
-    return false;
-  }
+bool ThreadTracer::arm(const SqttRequest& req, std::string* err) {
   if (req.dispatches <= 0 || req.dispatches > 64) {
     if (err) *err = "dispatches must be 1..64";
     return false;
@@ -174,35 +170,48 @@ bool ThreadTracer::start(const SqttRequest& req, std::string* err) {
     if (err) *err = "cannot create output directory '" + req.outDir + "'";
     return false;
   }
-  std::vector<uint64_t> ctxs;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    if (active_) {
-      if (err) *err = "a thread trace capture is already running";
-      return false;
-    }
-    try {
-      re_ = std::regex(req.kernelRegex.empty() ? std::string(".") : req.kernelRegex);
-    } catch (const std::regex_error& e) {
-      if (err) *err = std::string("bad kernel regex: ") + e.what();
-      return false;
-    }
-    anyKernel_ = req.kernelRegex.empty();
-    matchCache_.clear();
-    req_ = req;
-    remaining_ = req.dispatches;
-    caps_.clear();
-    for (const auto& [handle, ctx] : ctxOfAgent_) {
-      auto it = agentIndex_.find(handle);
-      if (req.agentIndex < 0 || (it != agentIndex_.end() && it->second == req.agentIndex)) ctxs.push_back(ctx);
-    }
-    if (ctxs.empty()) {
-      if (err) *err = "no thread trace context for agent " + std::to_string(req.agentIndex);
-      return false;
-    }
-    startNs_ = monoNow();
-    active_ = true;
+  std::lock_guard<std::mutex> g(mu_);
+  if (active_) {
+    if (err) *err = "a thread trace capture is already running";
+    return false;
   }
+  try {
+    re_ = std::regex(req.kernelRegex.empty() ? std::string(".") : req.kernelRegex);
+  } catch (const std::regex_error& e) {
+    if (err) *err = std::string("bad kernel regex: ") + e.what();
+    return false;
+  }
+  anyKernel_ = req.kernelRegex.empty();
+  matchCache_.clear();
+  req_ = req;
+  remaining_ = req.dispatches;
+  caps_.clear();
+  startNs_ = monoNow();
+  active_ = true;
+  return true;
+}
+
+bool ThreadTracer::testArm(const SqttRequest& req, const SqttParams& params, std::string* err) {
+  params_ = params;
+  startedCtx_.clear();
+  return arm(req, err);
+}
+
+bool ThreadTracer::start(const SqttRequest& req, std::string* err) {
+  if (!configured_) {
+    if (err) *err = "thread trace not configured (preinit with thread_trace enabled)";
+    return false;
+  }
+  std::vector<uint64_t> ctxs;
+  for (const auto& [handle, ctx] : ctxOfAgent_) {
+    auto it = agentIndex_.find(handle);
+    if (req.agentIndex < 0 || (it != agentIndex_.end() && it->second == req.agentIndex)) ctxs.push_back(ctx);
+  }
+  if (ctxs.empty()) {
+    if (err) *err = "no thread trace context for agent " + std::to_string(req.agentIndex);
+    return false;
+  }
+  if (!arm(req, err)) return false;
   startedCtx_.clear();
   for (uint64_t c : ctxs) {
     auto s = rocprofiler_start_context(rocprofiler_context_id_t{c});

@@ -64,11 +64,15 @@ class ThreadTracer {
 
   // Arms a capture and starts the trace contexts.
   bool start(const SqttRequest& req, std::string* err);
+  bool arm(const SqttRequest& req, std::string* err);  // state of a new capture (mu_ not held)
   // Waits until the requested dispatches have been traced and their data
   // has arrived (or timeoutMs passes), stops the contexts, writes the files
   // and returns the index (also written as <outDir>/sqtt_index_<pid>.json).
   Json finish(int timeoutMs, std::string* err);
   bool active() const { return active_; }
+  // Testing (CPU): arm a capture with these parameters without rocprofiler
+  // contexts; the callbacks are then driven by hand.
+  bool testArm(const SqttRequest& req, const SqttParams& params, std::string* err);
 
   // --- rocprofiler callbacks ---
   int onDispatch(uint64_t agentHandle, uint64_t kernelId, uint64_t dispatchId, uint64_t correlationId,
