@@ -212,7 +212,9 @@ bool Daemon::start(std::string* err) {
       return req.contains(k) && req.at(k).isNumber() ? req.at(k).asInt() : d;
     };
     const int n = static_cast<int>(std::clamp<int64_t>(geti("dispatches", 1), 1, 64));
-    const int timeoutMs = static_cast<int>(std::clamp<int64_t>(geti("timeout_ms", 10000), 100, 120000));
+    // below the registry's 60 s keepalive: the agent's control thread is
+    // busy for the whole capture
+    const int timeoutMs = static_cast<int>(std::clamp<int64_t>(geti("timeout_ms", 10000), 100, 45000));
     const std::string re = req.contains("kernel_regex") && req.at("kernel_regex").isString()
                                ? req.at("kernel_regex").asString()
                                : "";

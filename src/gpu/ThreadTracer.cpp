@@ -186,6 +186,7 @@ bool ThreadTracer::arm(const SqttRequest& req, std::string* err) {
   req_ = req;
   remaining_ = req.dispatches;
   caps_.clear();
+  ++gen_;
   startNs_ = monoNow();
   active_ = true;
   return true;
@@ -249,7 +250,7 @@ int ThreadTracer::onDispatch(uint64_t agentHandle, uint64_t kernelId, uint64_t d
   auto ai = agentIndex_.find(agentHandle);
   c.agentIndex = ai == agentIndex_.end() ? -1 : ai->second;
   c.armedNs = monoNow();
-  *userdata = caps_.size() + 1;  // 0 = not ours
+  *userdata = (gen_ << 16) | (caps_.size() + 1);  // index 0 = not ours
   caps_.push_back(std::move(c));
   --remaining_;
   return 1;
@@ -257,8 +258,9 @@ int ThreadTracer::onDispatch(uint64_t agentHandle, uint64_t kernelId, uint64_t d
 
 void ThreadTracer::onShaderData(uint64_t, int64_t se, const void* data, size_t n, uint64_t userdata) {
   std::lock_guard<std::mutex> g(mu_);
-  if (userdata == 0 || userdata > caps_.size()) return;
-  Capture& c = caps_[userdata - 1];
+  const uint64_t i = userdata & 0xffff;
+  if ((userdata >> 16) != gen_ || i == 0 || i > caps_.size()) return;
+  Capture& c = caps_[i - 1];
   c.seData[se].append(static_cast<const char*>(data), n);
   c.lastDataNs = monoNow();
   cv_.notify_all();

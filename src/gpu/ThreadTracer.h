@@ -118,6 +118,7 @@ class ThreadTracer {
   bool anyKernel_ = true;
   std::map<uint64_t, bool> matchCache_;  // kernel id -> name matches
   int remaining_ = 0;
+  uint64_t gen_ = 0;  // capture generation, in the shader userdata: late data of an old capture is dropped
   std::vector<Capture> caps_;
   std::vector<uint64_t> startedCtx_;
   uint64_t startNs_ = 0;
