@@ -105,3 +105,38 @@ def test_sqtt_several_shader_engines(native_built, tmp_path):
     print(ses, [s["bytes"] for s in d["shader_engines"]])
     assert d["complete"] and ses == [0, 1, 2, 3], d
     assert all(s["bytes"] > 0 for s in d["shader_engines"]), d
+
+
+def test_sqtt_with_kernel_trace_and_sampling(native_built, tmp_path):
+    """Every in-process service at once: kernel dispatch tracing, SQTT and
+    the 1 kHz counter agent.  The SQTT capture lands inside a kernel trace,
+    whose records still cover the traced dispatch."""
+    out = str(tmp_path / "sqtt")
+    res = _run(f"""
+        from dynolog_amd import agent
+        agent.preinit(kernel_trace=True, thread_trace=True)
+        import json, time, torch
+        torch.cuda.set_device(0)
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        y = x @ x; torch.cuda.synchronize()
+        kt = agent.KernelTrace().start()
+        tt = agent.ThreadTrace({out!r}, kernel_regex="Cijk", dispatches=1).start()
+        for _ in range(5):
+            y = x @ x
+        torch.cuda.synchronize()
+        idx = tt.finish(timeout_s=20)
+        for _ in range(5):
+            y = x @ x
+        torch.cuda.synchronize()
+        kt.stop()
+        summ = kt.summary(top=5)
+        time.sleep(0.2)
+        st = a.stats()
+        a.stop()
+        print("RESULT " + json.dumps(dict(idx=idx, summ=summ, st=st)))
+    """, timeout=300)
+    idx, summ, st = res["idx"], res["summ"], res["st"]
+    assert idx["traced"] == 1 and idx["dispatches"][0]["shader_engines"][0]["bytes"] > 0, idx
+    assert summ["dispatches"] >= 10, summ
+    assert st["samples_failed"] == 0 and st["samples_taken"] > 0, st
