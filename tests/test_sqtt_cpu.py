@@ -26,7 +26,11 @@ def test_sqtt_capture_bookkeeping(native_built, tmp_path):
     assert se0[0]["bytes"] == 6 and se0[1]["bytes"] == 3 and d0["complete"], d0
     with open(os.path.join(tmp_path, se0[0]["file"]), "rb") as f:
         assert f.read() == b"AAAABB"  # chunks appended in order
-    assert idx["total_bytes"] == 6 + 3 + 5 + 1
+    # the host-memory cap (14 bytes here) drops the last chunk: SE 1 of the
+    # second dispatch is missing and that dispatch is marked incomplete
+    assert idx["total_bytes"] == 6 + 3 + 5
+    assert not d1["complete"] and d1["dropped_bytes"] == 1, d1
+    assert [s["shader_engine"] for s in d1["shader_engines"]] == [0]
     (co,) = idx["code_objects"]  # only the traced kernels' object
     assert co["code_object_id"] == 7 and co["uri"].startswith("memory://")
     with open(os.path.join(tmp_path, co["file"]), "rb") as f:
