@@ -13,6 +13,7 @@
 #include "common/Logging.h"
 #include "common/Sync.h"
 #include "gpu/KernelCounters.h"
+#include "gpu/DispatchCounters.h"
 #include "gpu/KernelTracer.h"
 #include "gpu/ThreadTracer.h"
 #include "gpu/ShmGather.h"
@@ -112,8 +113,9 @@ Agent* Agent::instance() {
   return a;
 }
 
-bool Agent::preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace, bool threadTrace) {
-  return RocprofRuntime::get().preinit(agentIndices, err, kernelTrace, threadTrace);
+bool Agent::preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace, bool threadTrace,
+                    bool dispatchCounters) {
+  return RocprofRuntime::get().preinit(agentIndices, err, kernelTrace, threadTrace, dispatchCounters);
 }
 
 namespace {
@@ -1149,6 +1151,7 @@ void Agent::controlLoop() {
       c["endpoint"] = ctl_->endpoint().name();
       c["kernel_trace"] = KernelTracer::get().configured();
       c["thread_trace"] = ThreadTracer::get().configured();
+      c["dispatch_counters"] = DispatchCounters::get().configured();
       (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgAgentContext, c.dump()), cfg_.daemonEndpoint, 1, 0);
       nextKeepalive = now + 10'000'000'000ull;
     }
@@ -1192,6 +1195,12 @@ void Agent::controlLoop() {
           }
         }
         (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, res.dump()), msg->src, 3, 10000);
+        continue;
+      }
+      if (req.contains("op") && req.at("op").isString() && req.at("op").asString() == "dispatch_counters") {
+        (void)ctl_->syncSend(
+            ipc::Message::fromString(ipc::kMsgKernelTraceResult, dispatchCountersRequest(req, res).dump()),
+            msg->src, 3, 10000);
         continue;
       }
       if (req.contains("op") && req.at("op").isString() && req.at("op").asString() == "sqtt") {
@@ -1268,6 +1277,45 @@ Json Agent::sqttRequest(const Json& req, Json res) {
         unsigned long long bytes = 0;
         for (const auto& se : x.at("shader_engines").asArray()) bytes += static_cast<unsigned long long>(se.at("bytes").asInt());
         o["bytes"] = bytes;
+        d.push_back(o);
+      }
+    res["dispatches"] = d;
+  }
+  if (pauseHere) resume();
+  return res;
+}
+
+// "dispatch_counters" over the control channel: exact counters of the next N
+// matching dispatches (DispatchCounters), sampler paused; the reply carries
+// the per-kernel averages and at most 16 dispatches (datagram size).
+Json Agent::dispatchCountersRequest(const Json& req, Json res) {
+  auto& dc = DispatchCounters::get();
+  DispatchCountersRequest r;
+  r.kernelRegex = req.contains("kernel_regex") && req.at("kernel_regex").isString() ? req.at("kernel_regex").asString() : "";
+  r.dispatches = req.contains("dispatches") ? static_cast<int>(req.at("dispatches").asInt()) : 1;
+  r.counterSet = req.contains("counter_set") && req.at("counter_set").isString() ? req.at("counter_set").asString() : "lite";
+  r.agentIndex = sampler_ ? sampler_->agent().index : -1;
+  const int timeoutMs = req.contains("timeout_ms") ? static_cast<int>(req.at("timeout_ms").asInt()) : 10000;
+  const bool pauseHere = !paused_;
+  if (pauseHere) {
+    pause();
+    usleep(5000);  // the sampler loop stops its counting context within ~2 ms
+  }
+  std::string err;
+  if (!dc.start(r, &err)) {
+    res["status"] = "failed: " + err;
+  } else {
+    Json out = dc.finish(timeoutMs, &err);
+    res["status"] = err.empty() ? "ok" : "failed: " + err;
+    for (const char* k : {"counter_set", "requested", "counted", "kernels"})
+      if (out.contains(k)) res[k] = out.at(k);
+    Json d = Json::array();
+    if (out.contains("dispatches"))
+      for (const auto& x : out.at("dispatches").asArray()) {
+        if (d.size() >= 16) break;
+        Json o = x;
+        std::string k = o.at("kernel").asString();
+        if (k.size() > 160) o["kernel"] = k.substr(0, 157) + "...";
         d.push_back(o);
       }
     res["dispatches"] = d;

@@ -1,0 +1,64 @@
+"""Exact per-dispatch counters (src/gpu/DispatchCounters.h) on a real
+MI355X: rocprofiler-sdk dispatch counting on the next N matching kernels of
+a live process, with the same derived metrics as the 1 kHz sampler."""
+import json
+
+import pytest
+
+from test_gpu_agent import _run
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dispatch_counters_gemm_and_copy(native_built):
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit(dispatch_counters=True)
+        import json, time, torch
+        torch.cuda.set_device(0)
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
+        x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+        src = torch.ones(1 << 28, dtype=torch.float32, device="cuda")   # 1 GiB
+        dst = torch.empty_like(src)
+        y = x @ x; torch.add(src, 1.0, out=dst); torch.cuda.synchronize()
+        assert agent.DispatchCounters.configured()
+        dc = agent.DispatchCounters(kernel_regex="Cijk", dispatches=3).start()
+        for _ in range(5):
+            y = x @ x
+        torch.cuda.synchronize()
+        gemm = dc.finish(timeout_s=20)
+        dc = agent.DispatchCounters(kernel_regex="elementwise", dispatches=2).start()
+        for _ in range(3):
+            torch.add(src, 1.0, out=dst)
+        torch.cuda.synchronize()
+        copy = dc.finish(timeout_s=20)
+        prec = agent.DispatchCounters(kernel_regex="Cijk", dispatches=1, counter_set="precision").start()
+        y = x @ x; torch.cuda.synchronize()
+        prec = prec.finish(timeout_s=20)
+        time.sleep(0.2)
+        st = a.stats()
+        a.stop()
+        print("RESULT " + json.dumps(dict(gemm=gemm, copy=copy, prec=prec, st=st)))
+    """, timeout=300)
+    gemm, copy, prec, st = res["gemm"], res["copy"], res["prec"], res["st"]
+    print(json.dumps(gemm["kernels"], indent=1), json.dumps(copy["kernels"], indent=1))
+    assert "error" not in gemm and gemm["counted"] == 3, gemm
+    g = gemm["dispatches"][0]
+    flops = 2.0 * 8192 ** 3
+    # the bf16 MFMA rate from the counters matches the GEMM's FLOPs over its duration
+    tf_expected = flops / (g["duration_us"] * 1e-6) * 1e-12
+    assert g["derived"]["mfma_bf16_tflops"] == pytest.approx(tf_expected, rel=0.1), g
+    assert g["derived"]["mfma_util"] > 30 and g["derived"]["gpu_busy_pct"] > 90, g
+    assert g["counters"]["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 == pytest.approx(flops, rel=0.02), g
+    c = copy["dispatches"][0]
+    assert copy["counted"] == 2, copy
+    assert c["derived"]["mfma_util"] < 1 and c["derived"]["hbm_read_gbps"] > 1000, c
+    # 1 GiB read and 1 GiB written: the TCC request counts, priced as the
+    # sampler prices them, account for the bytes
+    rd = c["derived"]["hbm_read_gbps"] * c["duration_us"] * 1e3
+    wr = c["derived"]["hbm_write_gbps"] * c["duration_us"] * 1e3
+    print("copy bytes read %.3g written %.3g" % (rd, wr))
+    assert rd == pytest.approx(1 << 30, rel=0.25) and wr == pytest.approx(1 << 30, rel=0.25), c
+    p = prec["dispatches"][0]["derived"]
+    assert "fp32_active" in p and p["mfma_bf16_tflops"] > 100, prec
+    assert st["samples_failed"] == 0

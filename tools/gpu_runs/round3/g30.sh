@@ -1,0 +1,4 @@
+# round 3 g30: first exact per-dispatch counter captures (dispatch counting service)
+set -o pipefail
+O=gpurun_out/g30; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_dispatch_counters.py -m gpu -x -v -s --timeout 320 --timeout-method thread > $O/pytest_dcount.log 2>&1
