@@ -28,6 +28,8 @@ void GpuAgentRegistry::onContext(const Json& j, const std::string& src) {
   e.endpoint = j.contains("endpoint") && j.at("endpoint").isString() ? j.at("endpoint").asString() : src;
   e.kernelTrace = j.contains("kernel_trace") && j.at("kernel_trace").isBool() && j.at("kernel_trace").asBool();
   e.threadTrace = j.contains("thread_trace") && j.at("thread_trace").isBool() && j.at("thread_trace").asBool();
+  e.dispatchCounters = j.contains("dispatch_counters") && j.at("dispatch_counters").isBool() &&
+                       j.at("dispatch_counters").asBool();
   e.lastSeenNs = nowNsMonotonic();
   if (e.pid <= 0) return;
   std::lock_guard<std::mutex> g(mu_);
@@ -77,6 +79,7 @@ Json GpuAgentRegistry::listJson() {
     o["endpoint"] = e.endpoint;
     o["kernel_trace"] = e.kernelTrace;
     o["thread_trace"] = e.threadTrace;
+    o["dispatch_counters"] = e.dispatchCounters;
     o["last_seen_s"] = (now - e.lastSeenNs) * 1e-9;
     arr.push_back(o);
   }
@@ -88,11 +91,28 @@ Json GpuAgentRegistry::listJson() {
 Json GpuAgentRegistry::kernelTrace(const std::vector<int>& pids, int durationMs, int top,
                                    const std::string& chromeDir, const Sender& send, int slackMs) {
   auto targets = agents(pids);
-  Json out = Json::object();
   if (targets.empty()) {
+    Json out = Json::object();
     out["status"] = "failed: no GPU agents registered" + std::string(pids.empty() ? "" : " for these pids");
     return out;
   }
+  return ask(
+      targets,
+      [&](const GpuAgentEntry& a) {
+        Json req = Json::object();
+        req["duration_ms"] = durationMs;
+        req["top"] = top;
+        if (!chromeDir.empty())
+          req["chrome_path"] =
+              chromeDir + "/gpu_kernels_" + std::to_string(a.pid) + "_r" + std::to_string(a.rank) + ".json";
+        return req;
+      },
+      durationMs + slackMs, send);
+}
+
+Json GpuAgentRegistry::ask(const std::vector<GpuAgentEntry>& targets,
+                           const std::function<Json(const GpuAgentEntry&)>& makeReq, int waitMs,
+                           const Sender& send) {
   uint64_t id;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -102,12 +122,8 @@ Json GpuAgentRegistry::kernelTrace(const std::vector<int>& pids, int durationMs,
   Json sent = Json::array();
   size_t expected = 0;
   for (const auto& a : targets) {
-    Json req = Json::object();
+    Json req = makeReq(a);
     req["id"] = static_cast<unsigned long long>(id);
-    req["duration_ms"] = durationMs;
-    req["top"] = top;
-    if (!chromeDir.empty())
-      req["chrome_path"] = chromeDir + "/gpu_kernels_" + std::to_string(a.pid) + "_r" + std::to_string(a.rank) + ".json";
     if (send("gktr", req.dump(), a.endpoint)) {
       ++expected;
       sent.push_back(a.pid);
@@ -116,13 +132,13 @@ Json GpuAgentRegistry::kernelTrace(const std::vector<int>& pids, int durationMs,
   std::vector<Json> got;
   {
     std::unique_lock<std::mutex> lk(mu_);
-    condWaitFor(cv_, lk, std::chrono::milliseconds(durationMs + slackMs),
-                 [&] { return results_[id].size() >= expected; });
+    condWaitFor(cv_, lk, std::chrono::milliseconds(waitMs), [&] { return results_[id].size() >= expected; });
     got = std::move(results_[id]);
     results_.erase(id);
   }
   Json res = Json::array();
   for (auto& r : got) res.push_back(r);
+  Json out = Json::object();
   out["status"] = got.size() == expected ? "ok" : "partial";
   out["requested"] = sent;
   out["results"] = res;
@@ -131,51 +147,55 @@ Json GpuAgentRegistry::kernelTrace(const std::vector<int>& pids, int durationMs,
 
 Json GpuAgentRegistry::threadTrace(const std::vector<int>& pids, const std::string& kernelRegex, int dispatches,
                                    const std::string& outDir, int timeoutMs, const Sender& send, int slackMs) {
-  Json out = Json::object();
   std::vector<GpuAgentEntry> targets;
   for (const auto& a : agents(pids))
     if (a.threadTrace) targets.push_back(a);
   if (targets.empty()) {
+    Json out = Json::object();
     out["status"] = "failed: no GPU agent with thread trace registered" +
                     std::string(pids.empty() ? "" : " for these pids") +
                     " (the process must call agent.preinit(thread_trace=True))";
     return out;
   }
-  uint64_t id;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    id = nextId_++;
-    results_[id] = {};
+  return ask(
+      targets,
+      [&](const GpuAgentEntry& a) {
+        Json req = Json::object();
+        req["op"] = "sqtt";
+        req["kernel_regex"] = kernelRegex;
+        req["dispatches"] = dispatches;
+        req["timeout_ms"] = timeoutMs;
+        req["out_dir"] = outDir + "/pid" + std::to_string(a.pid) + "_r" + std::to_string(a.rank);
+        return req;
+      },
+      timeoutMs + slackMs, send);
+}
+
+Json GpuAgentRegistry::dispatchCounters(const std::vector<int>& pids, const std::string& kernelRegex, int dispatches,
+                                        const std::string& counterSet, int timeoutMs, const Sender& send,
+                                        int slackMs) {
+  std::vector<GpuAgentEntry> targets;
+  for (const auto& a : agents(pids))
+    if (a.dispatchCounters) targets.push_back(a);
+  if (targets.empty()) {
+    Json out = Json::object();
+    out["status"] = "failed: no GPU agent with dispatch counters registered" +
+                    std::string(pids.empty() ? "" : " for these pids") +
+                    " (the process must call agent.preinit(dispatch_counters=True))";
+    return out;
   }
-  Json sent = Json::array();
-  size_t expected = 0;
-  for (const auto& a : targets) {
-    Json req = Json::object();
-    req["id"] = static_cast<unsigned long long>(id);
-    req["op"] = "sqtt";
-    req["kernel_regex"] = kernelRegex;
-    req["dispatches"] = dispatches;
-    req["timeout_ms"] = timeoutMs;
-    req["out_dir"] = outDir + "/pid" + std::to_string(a.pid) + "_r" + std::to_string(a.rank);
-    if (send("gktr", req.dump(), a.endpoint)) {
-      ++expected;
-      sent.push_back(a.pid);
-    }
-  }
-  std::vector<Json> got;
-  {
-    std::unique_lock<std::mutex> lk(mu_);
-    condWaitFor(cv_, lk, std::chrono::milliseconds(timeoutMs + slackMs),
-                [&] { return results_[id].size() >= expected; });
-    got = std::move(results_[id]);
-    results_.erase(id);
-  }
-  Json res = Json::array();
-  for (auto& r : got) res.push_back(r);
-  out["status"] = got.size() == expected ? "ok" : "partial";
-  out["requested"] = sent;
-  out["results"] = res;
-  return out;
+  return ask(
+      targets,
+      [&](const GpuAgentEntry&) {
+        Json req = Json::object();
+        req["op"] = "dispatch_counters";
+        req["kernel_regex"] = kernelRegex;
+        req["dispatches"] = dispatches;
+        req["counter_set"] = counterSet;
+        req["timeout_ms"] = timeoutMs;
+        return req;
+      },
+      timeoutMs + slackMs, send);
 }
 
 std::vector<Json> GpuAgentRegistry::counterTracks(uint64_t t0Ns, uint64_t t1Ns, int device,

@@ -6,6 +6,7 @@
 //   agent  -> daemon  "gktd" {id, pid, rank, status, summary}              (result)
 //   daemon -> agent   "gktr" {id, op:"sqtt", kernel_regex, dispatches, out_dir, timeout_ms}
 //                                                    (SQTT capture, answered with "gktd")
+//   daemon -> agent   "gktr" {id, op:"dispatch_counters", kernel_regex, dispatches, counter_set, timeout_ms}
 //
 // The registry plays the role LibkinetoConfigManager plays for libkineto
 // processes (reference LibkinetoConfigManager.cpp:146-191: registration on
@@ -30,6 +31,7 @@ struct GpuAgentEntry {
   std::string endpoint;
   bool kernelTrace = false;
   bool threadTrace = false;
+  bool dispatchCounters = false;
   uint64_t lastSeenNs = 0;
 };
 
@@ -53,6 +55,10 @@ class GpuAgentRegistry {
   // collect their summaries (waits up to timeoutMs + slackMs).
   Json threadTrace(const std::vector<int>& pids, const std::string& kernelRegex, int dispatches,
                    const std::string& outDir, int timeoutMs, const Sender& send, int slackMs = 5000);
+  // Ask every matching agent for exact counters of its next `dispatches`
+  // kernels matching `kernelRegex` (DispatchCounters) and collect the replies.
+  Json dispatchCounters(const std::vector<int>& pids, const std::string& kernelRegex, int dispatches,
+                        const std::string& counterSet, int timeoutMs, const Sender& send, int slackMs = 5000);
   // Ask every live agent for its 1 kHz counter tracks of [t0Ns, t1Ns]
   // (CLOCK_MONOTONIC) of GPU `device` (-1: all); aggregators write them to
   // "<pathPrefix><pid>.json".  Returns the events of every agent that had
@@ -62,6 +68,10 @@ class GpuAgentRegistry {
 
  private:
   void gcLocked(uint64_t now);
+  // one "gktr" request per target (makeReq builds it; the id is added) and
+  // the replies collected for up to waitMs
+  Json ask(const std::vector<GpuAgentEntry>& targets, const std::function<Json(const GpuAgentEntry&)>& makeReq,
+           int waitMs, const Sender& send);
   std::mutex mu_;
   std::condition_variable cv_;
   std::map<int, GpuAgentEntry> agents_;     // by pid*1000+rank
