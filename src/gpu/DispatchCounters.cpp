@@ -133,6 +133,10 @@ bool DispatchCounters::buildConfigs(const std::vector<std::string>& names, std::
     AgentCfg a;
     a.index = ai.index;
     a.consts = makeAgentConsts(ai);
+    // as the sampler prices them (Agent.cpp): without the size-class counter
+    // a write request is the dominant 64-B class
+    if (DC_TCC_EA0_WRREQ_64B < static_cast<int>(names.size()) && names[DC_TCC_EA0_WRREQ_64B].empty())
+      a.consts.hbm_write_bytes_per_req = 64.0f;
     std::vector<rocprofiler_counter_id_t> want;
     for (size_t i = 0; i < names.size(); ++i) {
       if (names[i].empty()) continue;
