@@ -110,9 +110,14 @@ bool DispatchCounters::configure(std::string* err) {
 
 bool DispatchCounters::buildConfigs(const std::vector<std::string>& names, std::string* err) {
   agents_.clear();
-  recordSlot_.clear();
   for (const auto& ai : RocprofRuntime::get().agents()) {
     if (req_.agentIndex >= 0 && ai.index != req_.agentIndex) continue;
+    const auto key = std::make_pair(req_.counterSet, ai.index);
+    auto hit = cache_.find(key);
+    if (hit != cache_.end()) {
+      agents_[ai.handle] = hit->second;
+      continue;
+    }
     rocprofiler_agent_id_t aid{ai.handle};
     std::vector<rocprofiler_counter_id_t> ids;
     rocprofiler_iterate_agent_supported_counters(
@@ -155,6 +160,7 @@ bool DispatchCounters::buildConfigs(const std::vector<std::string>& names, std::
       return false;
     }
     a.config = cfg.handle;
+    cache_[key] = a;
     agents_[ai.handle] = std::move(a);
   }
   if (agents_.empty()) {
@@ -244,16 +250,16 @@ uint64_t DispatchCounters::onDispatch(uint64_t agentHandle, uint64_t kernelId, u
   return a->second.config;
 }
 
-int DispatchCounters::slotOfRecord(const AgentCfg& a, uint64_t recordId) {
-  auto it = recordSlot_.find(recordId);
-  if (it != recordSlot_.end()) return it->second;
+int DispatchCounters::slotOfRecord(AgentCfg& a, uint64_t recordId) {
+  auto it = a.slotOfRecord.find(recordId);
+  if (it != a.slotOfRecord.end()) return it->second;
   rocprofiler_counter_id_t cid{};
   int slot = -1;
   if (rocprofiler_query_record_counter_id(recordId, &cid) == ROCPROFILER_STATUS_SUCCESS) {
     auto s = a.slotOfCounter.find(cid.handle);
     if (s != a.slotOfCounter.end()) slot = s->second;
   }
-  recordSlot_[recordId] = slot;
+  a.slotOfRecord[recordId] = slot;
   return slot;
 }
 
@@ -264,8 +270,8 @@ void DispatchCounters::onRecords(uint64_t userdata, uint64_t kernelId, uint64_t 
   const uint64_t i = userdata & 0xffff;
   if ((userdata >> 16) != gen_ || i == 0 || i > counted_.size()) return;
   Counted& c = counted_[i - 1];
-  const AgentCfg* a = nullptr;
-  for (const auto& [h, cfg] : agents_)
+  AgentCfg* a = nullptr;
+  for (auto& [h, cfg] : agents_)
     if (cfg.index == c.agentIndex) a = &cfg;
   if (!a) return;
   for (size_t r = 0; r < n; ++r) {
@@ -295,7 +301,6 @@ bool DispatchCounters::testArm(const DispatchCountersRequest& req, const std::ve
                                uint32_t pass, const DynoAgentConsts& consts, std::string* err) {
   std::lock_guard<std::mutex> g(mu_);
   agents_.clear();
-  recordSlot_.clear();
   AgentCfg a;
   a.index = 0;
   a.config = 1;

@@ -80,11 +80,12 @@ class DispatchCounters {
     int index = -1;
     uint64_t config = 0;                   // counter config of the armed set
     std::map<uint64_t, int> slotOfCounter;  // counter id -> slot
+    std::map<uint64_t, int> slotOfRecord;   // record instance id -> slot (cache)
     DynoAgentConsts consts{};
   };
   bool arm(const DispatchCountersRequest& req, std::string* err);
   bool buildConfigs(const std::vector<std::string>& names, std::string* err);
-  int slotOfRecord(const AgentCfg& a, uint64_t recordId);
+  static int slotOfRecord(AgentCfg& a, uint64_t recordId);
 
   mutable std::mutex mu_;
   std::condition_variable cv_;
@@ -93,7 +94,9 @@ class DispatchCounters {
   uint64_t ctx_ = 0;
   std::map<uint64_t, std::string> names_;  // kernel id -> symbol
   std::map<uint64_t, AgentCfg> agents_;    // agent handle -> armed config
-  std::map<uint64_t, int> recordSlot_;     // record counter id -> slot (all agents share ids)
+  // counter configs already created: (set, agent index) -> config (a capture
+  // of a set seen before reuses it instead of creating another)
+  std::map<std::pair<std::string, int>, AgentCfg> cache_;
   // current capture
   DispatchCountersRequest req_;
   std::vector<std::string> slotNames_;
