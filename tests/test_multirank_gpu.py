@@ -127,13 +127,23 @@ def test_rccl_collective_gather_across_fake_hosts(native_built, mode, world, nod
            os.path.join(REPO, "bench.py"),
            "--gpus", str(world), "--model", "small", "--seq-len", "1024", "--steps", "4",
            "--warmup", "2", "--gather-mode", mode, "--ab-rounds", "1", "--ab-steps", "2",
-           "--host-pmu", "off", "--no-agent-baseline", "off"]
+           "--host-pmu", "off"]
+    # the 2-rank gather case keeps the no-agent baseline children (an RCCL
+    # group of their own before and after), as the driver's runs do
+    children = mode == "gather" and world == 2 and not nodes
+    if not children:
+        cmd += ["--no-agent-baseline", "off"]
     r = _run_logged(cmd, env, 300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["dist_backend"] == "nccl", out.get("dist_backend")
+    if children:
+        runs = out["no_agent_runs"]
+        assert [x["tag"] for x in runs] == ["before", "after"], runs
+        assert all(x.get("rc") == 0 and x.get("ms_per_step", 0) > 0 for x in runs), runs
+        assert out["overhead_vs_no_agent_pct"] is not None
     assert "gather_fallback" not in out and out["config"]["gather"] == mode, out
     group = world // nodes if nodes else world
     assert out["gather_group_size"] == group
