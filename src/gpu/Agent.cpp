@@ -13,6 +13,7 @@
 #include "common/Logging.h"
 #include "common/Sync.h"
 #include "gpu/KernelCounters.h"
+#include "gpu/CommTracer.h"
 #include "gpu/DispatchCounters.h"
 #include "gpu/KernelTracer.h"
 #include "gpu/ThreadTracer.h"
@@ -114,8 +115,8 @@ Agent* Agent::instance() {
 }
 
 bool Agent::preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace, bool threadTrace,
-                    bool dispatchCounters) {
-  return RocprofRuntime::get().preinit(agentIndices, err, kernelTrace, threadTrace, dispatchCounters);
+                    bool dispatchCounters, bool commTrace) {
+  return RocprofRuntime::get().preinit(agentIndices, err, kernelTrace, threadTrace, dispatchCounters, commTrace);
 }
 
 namespace {
@@ -1152,6 +1153,7 @@ void Agent::controlLoop() {
       c["kernel_trace"] = KernelTracer::get().configured();
       c["thread_trace"] = ThreadTracer::get().configured();
       c["dispatch_counters"] = DispatchCounters::get().configured();
+      c["comm_trace"] = CommTracer::get().configured();
       (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgAgentContext, c.dump()), cfg_.daemonEndpoint, 1, 0);
       nextKeepalive = now + 10'000'000'000ull;
     }
@@ -1195,6 +1197,11 @@ void Agent::controlLoop() {
           }
         }
         (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, res.dump()), msg->src, 3, 10000);
+        continue;
+      }
+      if (req.contains("op") && req.at("op").isString() && req.at("op").asString() == "comm_trace") {
+        (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgKernelTraceResult, commTraceRequest(req, res).dump()),
+                             msg->src, 3, 10000);
         continue;
       }
       if (req.contains("op") && req.at("op").isString() && req.at("op").asString() == "dispatch_counters") {
@@ -1321,6 +1328,35 @@ Json Agent::dispatchCountersRequest(const Json& req, Json res) {
     res["dispatches"] = d;
   }
   if (pauseHere) resume();
+  return res;
+}
+
+// "comm_trace" over the control channel: this process's RCCL collectives for
+// duration_ms (CommTracer), with their RCCL kernels' GPU time when kernel
+// tracing is configured too (a kernel trace runs over the same window).
+Json Agent::commTraceRequest(const Json& req, Json res) {
+  auto& ct = CommTracer::get();
+  auto& kt = KernelTracer::get();
+  const int dur = req.contains("duration_ms") ? static_cast<int>(req.at("duration_ms").asInt()) : 1000;
+  const int last = req.contains("last") ? static_cast<int>(req.at("last").asInt()) : 16;
+  std::string err;
+  if (!ct.start(&err)) {
+    res["status"] = "failed: " + err;
+    return res;
+  }
+  const bool withKernels = kt.configured() && !kt.active() && kt.start(&err);
+  const uint64_t end = monoNs() + static_cast<uint64_t>(std::max(dur, 1)) * 1000000ull;
+  while (!stopFlag_ && monoNs() < end) usleep(10000);
+  if (withKernels) {
+    usleep(20000);  // the window's last collectives complete
+    kt.stop(&err);
+  }
+  ct.stop(&err);
+  Json s = ct.summary(static_cast<size_t>(std::clamp(last, 0, 64)));
+  res["status"] = "ok";
+  for (const char* k : {"window_ms", "calls", "dropped", "gpu_time_by", "ops", "last_calls"})
+    if (s.contains(k)) res[k] = s.at(k);
+  res["kernel_trace"] = withKernels;
   return res;
 }
 

@@ -92,7 +92,7 @@ class Agent {
  public:
   static Agent* instance();
   static bool preinit(const std::vector<int>& agentIndices, std::string* err, bool kernelTrace = false,
-                      bool threadTrace = false, bool dispatchCounters = false);
+                      bool threadTrace = false, bool dispatchCounters = false, bool commTrace = false);
 
   bool start(const AgentConfig& cfg, const void* ncclUniqueId, size_t idLen, std::string* err);
   // Enqueue the rank-0 gather on `stream` (nullptr = legacy default stream).
@@ -136,6 +136,7 @@ class Agent {
   void controlLoop();
   Json sqttRequest(const Json& req, Json res);
   Json dispatchCountersRequest(const Json& req, Json res);
+  Json commTraceRequest(const Json& req, Json res);
   bool flushBatch(int nstaged, std::string* err);
   void consumerLoop();
   void logInterval();

@@ -58,7 +58,7 @@ class RocprofRuntime {
   // threadTrace: also configure on-demand SQTT capture (ThreadTracer)
   // dispatchCounters: also configure on-demand per-dispatch counters (DispatchCounters)
   bool preinit(const std::vector<int>& devices, std::string* err, bool kernelTrace = false,
-               bool threadTrace = false, bool dispatchCounters = false);
+               bool threadTrace = false, bool dispatchCounters = false, bool commTrace = false);
   // Discovery path (ROCP_TOOL_LIBRARIES, set by the Python preinit() when
   // importing torch would initialise HIP first): rocprofiler-sdk loads this
   // library at HSA init and calls the exported rocprofiler_configure, which
@@ -89,6 +89,7 @@ class RocprofRuntime {
   bool kernelTrace_ = false;
   bool threadTrace_ = false;
   bool dispatchCounters_ = false;
+  bool commTrace_ = false;
   std::vector<AgentInfo> agents_;
   std::map<int, std::unique_ptr<Ctx>> ctxs_;
   std::string err_;

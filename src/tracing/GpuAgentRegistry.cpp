@@ -30,6 +30,7 @@ void GpuAgentRegistry::onContext(const Json& j, const std::string& src) {
   e.threadTrace = j.contains("thread_trace") && j.at("thread_trace").isBool() && j.at("thread_trace").asBool();
   e.dispatchCounters = j.contains("dispatch_counters") && j.at("dispatch_counters").isBool() &&
                        j.at("dispatch_counters").asBool();
+  e.commTrace = j.contains("comm_trace") && j.at("comm_trace").isBool() && j.at("comm_trace").asBool();
   e.lastSeenNs = nowNsMonotonic();
   if (e.pid <= 0) return;
   std::lock_guard<std::mutex> g(mu_);
@@ -80,6 +81,7 @@ Json GpuAgentRegistry::listJson() {
     o["kernel_trace"] = e.kernelTrace;
     o["thread_trace"] = e.threadTrace;
     o["dispatch_counters"] = e.dispatchCounters;
+    o["comm_trace"] = e.commTrace;
     o["last_seen_s"] = (now - e.lastSeenNs) * 1e-9;
     arr.push_back(o);
   }
@@ -196,6 +198,30 @@ Json GpuAgentRegistry::dispatchCounters(const std::vector<int>& pids, const std:
         return req;
       },
       timeoutMs + slackMs, send);
+}
+
+Json GpuAgentRegistry::commTrace(const std::vector<int>& pids, int durationMs, int last, const Sender& send,
+                                 int slackMs) {
+  std::vector<GpuAgentEntry> targets;
+  for (const auto& a : agents(pids))
+    if (a.commTrace) targets.push_back(a);
+  if (targets.empty()) {
+    Json out = Json::object();
+    out["status"] = "failed: no GPU agent with RCCL tracing registered" +
+                    std::string(pids.empty() ? "" : " for these pids") +
+                    " (the process must call agent.preinit(comm_trace=True))";
+    return out;
+  }
+  return ask(
+      targets,
+      [&](const GpuAgentEntry&) {
+        Json req = Json::object();
+        req["op"] = "comm_trace";
+        req["duration_ms"] = durationMs;
+        req["last"] = last;
+        return req;
+      },
+      durationMs + slackMs, send);
 }
 
 std::vector<Json> GpuAgentRegistry::counterTracks(uint64_t t0Ns, uint64_t t1Ns, int device,

@@ -7,6 +7,7 @@
 //   daemon -> agent   "gktr" {id, op:"sqtt", kernel_regex, dispatches, out_dir, timeout_ms}
 //                                                    (SQTT capture, answered with "gktd")
 //   daemon -> agent   "gktr" {id, op:"dispatch_counters", kernel_regex, dispatches, counter_set, timeout_ms}
+//   daemon -> agent   "gktr" {id, op:"comm_trace", duration_ms, last}
 //
 // The registry plays the role LibkinetoConfigManager plays for libkineto
 // processes (reference LibkinetoConfigManager.cpp:146-191: registration on
@@ -32,6 +33,7 @@ struct GpuAgentEntry {
   bool kernelTrace = false;
   bool threadTrace = false;
   bool dispatchCounters = false;
+  bool commTrace = false;
   uint64_t lastSeenNs = 0;
 };
 
@@ -59,6 +61,9 @@ class GpuAgentRegistry {
   // kernels matching `kernelRegex` (DispatchCounters) and collect the replies.
   Json dispatchCounters(const std::vector<int>& pids, const std::string& kernelRegex, int dispatches,
                         const std::string& counterSet, int timeoutMs, const Sender& send, int slackMs = 5000);
+  // Ask every matching agent for its RCCL collectives over durationMs
+  // (CommTracer) and collect the replies.
+  Json commTrace(const std::vector<int>& pids, int durationMs, int last, const Sender& send, int slackMs = 5000);
   // Ask every live agent for its 1 kHz counter tracks of [t0Ns, t1Ns]
   // (CLOCK_MONOTONIC) of GPU `device` (-1: all); aggregators write them to
   // "<pathPrefix><pid>.json".  Returns the events of every agent that had
