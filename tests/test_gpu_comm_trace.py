@@ -85,7 +85,10 @@ def test_gpucomms_rpc_through_agent(native_built, tmp_path):
             p = subprocess.Popen([sys.executable, "-c", code], env=penv, stdout=subprocess.PIPE,
                                  stderr=subprocess.PIPE, text=True)
             try:
-                pid = int(p.stdout.readline().split()[1])
+                line = p.stdout.readline()
+                while line and not line.startswith("PID"):  # RCCL prints its version first
+                    line = p.stdout.readline()
+                pid = int(line.split()[1])
                 deadline = time.time() + 60
                 ags = []
                 while time.time() < deadline:
