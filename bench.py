@@ -73,6 +73,9 @@ def parse_args(argv=None):
                    help="distinct synthetic batches cycled through the steps")
     p.add_argument("--phases", action="store_true",
                    help="mark forward/backward/optimizer on the GPU stream and report per-phase metrics")
+    p.add_argument("--comm-trace", action="store_true",
+                   help="after the timed region, trace one more step's RCCL collectives "
+                        "(agent.CommTrace: op, size, ranks, host time) into the result line")
     p.add_argument("--kernel-trace-ready", action="store_true",
                    help="also configure (idle) on-demand kernel tracing, to price its queue interception")
     p.add_argument("--skip-baseline", action="store_true")
@@ -173,7 +176,7 @@ def main(argv=None) -> int:
         else:
             idx = dagent.agent_index_for_local_rank(int(os.environ.get("LOCAL_RANK", "0")))
             want = None if idx is None else [idx]
-        dagent.preinit(want, kernel_trace=args.kernel_trace_ready)
+        dagent.preinit(want, kernel_trace=args.kernel_trace_ready, comm_trace=args.comm_trace)
 
     import torch
     from dynolog_amd.models.llama import CONFIGS, build_llama, lm_loss
@@ -382,6 +385,14 @@ def main(argv=None) -> int:
         window_s = (m1 - m0) * 1e-9 if ag is not None else meas_s
         value = total_samples / window_s if window_s > 0 else 0.0
         tokens = B * S * env.world * args.steps
+        collectives = None
+        if args.comm_trace and use_agent:
+            # one more step, outside every timed window, with its RCCL calls traced
+            ct = dagent.CommTrace().start()
+            train_step()
+            torch.cuda.synchronize()
+            ct.stop()
+            collectives = ct.summary(last=0)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -438,6 +449,8 @@ def main(argv=None) -> int:
                     out["paused_vs_no_agent_pct"] = round((base_s / args.steps * 1e3 / no_agent_ms - 1.0) * 100.0, 3)
         if torch.distributed.is_initialized():
             out["dist_backend"] = torch.distributed.get_backend()
+        if collectives is not None:
+            out["collectives_per_step"] = collectives["ops"]
         if ag is not None:
             # ranks per gather group (= n_gpus on one node; one group per node otherwise)
             out["gather_group_size"] = ag.gather_world

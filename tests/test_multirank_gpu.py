@@ -133,12 +133,20 @@ def test_rccl_collective_gather_across_fake_hosts(native_built, mode, world, nod
     children = mode == "gather" and world == 2 and not nodes
     if not children:
         cmd += ["--no-agent-baseline", "off"]
+    comm = mode == "gather" and world == 4 and not nodes
+    if comm:  # one more step with its RCCL calls traced (agent.CommTrace)
+        cmd += ["--comm-trace"]
     r = _run_logged(cmd, env, 300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["dist_backend"] == "nccl", out.get("dist_backend")
+    if comm:
+        ops = {o["op"]: o for o in out["collectives_per_step"]}
+        # DDP's gradient all-reduces and the agent's own gather, on 4-rank communicators
+        assert ops["AllReduce"]["nranks"] == world and ops["AllReduce"]["calls"] >= 1, ops
+        assert ops["AllReduce"]["bytes"] > 0 and ops["Gather"]["nranks"] == world, ops
     if children:
         runs = out["no_agent_runs"]
         assert [x["tag"] for x in runs] == ["before", "after"], runs
