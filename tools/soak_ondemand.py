@@ -1,0 +1,110 @@
+"""Soak of the on-demand in-process GPU services next to the 1 kHz agent:
+a bf16 GEMM / elementwise training-like loop runs for --minutes while, every
+--every seconds, one exact dispatch-counter capture, one SQTT capture (its
+files removed afterwards) and one RCCL collective trace (a 1-rank NCCL group)
+run in turn.  Host RSS, GPU memory in use and the agent's sample counters are
+recorded after each round; the summary says whether they stayed bounded.
+
+    python tools/soak_ondemand.py --minutes 3 --out gpurun_out/soak_ondemand.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def rss_mb() -> float:
+    with open("/proc/self/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1]) / 1024.0
+    return 0.0
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--minutes", type=float, default=3.0)
+    ap.add_argument("--every", type=float, default=5.0)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+
+    from dynolog_amd import agent
+    agent.preinit([0], kernel_trace=True, thread_trace=True, dispatch_counters=True, comm_trace=True)
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29659")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    ag = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",))
+    x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    g = torch.ones(16 << 20, device="cuda")
+    out = torch.empty(16 << 20, device="cuda")
+
+    def work():
+        for _ in range(8):
+            y = x @ x  # noqa: F841
+        torch.add(g, 1.0, out=out)
+        dist.all_gather_into_tensor(out, g)
+        torch.cuda.synchronize()
+        ag.step()
+
+    rounds = []
+    end = time.time() + a.minutes * 60
+    next_round = time.time() + a.every
+    kinds = ["dispatch_counters", "sqtt", "comm_trace"]
+    k = 0
+    while time.time() < end:
+        work()
+        if time.time() < next_round:
+            continue
+        kind = kinds[k % len(kinds)]
+        k += 1
+        t0 = time.time()
+        ok = False
+        if kind == "dispatch_counters":
+            dc = agent.DispatchCounters(kernel_regex="Cijk", dispatches=4).start()
+            work()
+            ok = dc.finish(timeout_s=20).get("counted") == 4
+        elif kind == "sqtt":
+            d = tempfile.mkdtemp(prefix="soak_sqtt_")
+            tt = agent.ThreadTrace(d, kernel_regex="Cijk", dispatches=1).start()
+            work()
+            ok = tt.finish(timeout_s=20).get("traced") == 1
+            shutil.rmtree(d, ignore_errors=True)
+        else:
+            with agent.CommTrace() as ct:
+                work()
+            ok = any(o["op"] == "AllGather" for o in ct.summary(last=0)["ops"])
+        st = ag.stats()
+        rounds.append({"kind": kind, "ok": ok, "s": round(time.time() - t0, 3), "rss_mb": round(rss_mb(), 1),
+                       "gpu_mb": round(torch.cuda.memory_allocated() / 2**20, 1),
+                       "samples_taken": st["samples_taken"], "samples_failed": st["samples_failed"]})
+        print(json.dumps(rounds[-1]), flush=True)
+        next_round = time.time() + a.every
+    st = ag.stats()
+    ag.stop()
+    dist.destroy_process_group()
+    first = [r for r in rounds[: len(kinds)]]
+    last = [r for r in rounds[-len(kinds):]]
+    res = {"minutes": a.minutes, "rounds": len(rounds), "all_ok": all(r["ok"] for r in rounds),
+           "rss_mb_first": first[-1]["rss_mb"] if first else None, "rss_mb_last": last[-1]["rss_mb"] if last else None,
+           "rss_mb_max": max((r["rss_mb"] for r in rounds), default=None),
+           "gpu_mb_first": first[-1]["gpu_mb"] if first else None, "gpu_mb_last": last[-1]["gpu_mb"] if last else None,
+           "samples_taken": st["samples_taken"], "samples_failed": st["samples_failed"], "per_round": rounds}
+    print(json.dumps({k2: v for k2, v in res.items() if k2 != "per_round"}))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    return 0 if res["all_ok"] and st["samples_failed"] == 0 else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
