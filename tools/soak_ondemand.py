@@ -33,10 +33,14 @@ def main() -> int:
     ap.add_argument("--minutes", type=float, default=3.0)
     ap.add_argument("--every", type=float, default=5.0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--services", default="dispatch_counters,sqtt,comm_trace,kernel_trace",
+                    help="services configured at preinit and exercised (the rest idle / absent)")
     a = ap.parse_args()
 
     from dynolog_amd import agent
-    agent.preinit([0], kernel_trace=True, thread_trace=True, dispatch_counters=True, comm_trace=True)
+    svc = [x for x in a.services.split(",") if x]
+    agent.preinit([0], kernel_trace="kernel_trace" in svc, thread_trace="sqtt" in svc,
+                  dispatch_counters="dispatch_counters" in svc, comm_trace="comm_trace" in svc)
     import torch
     import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -59,7 +63,7 @@ def main() -> int:
     rounds = []
     end = time.time() + a.minutes * 60
     next_round = time.time() + a.every
-    kinds = ["dispatch_counters", "sqtt", "comm_trace"]
+    kinds = [x for x in ("dispatch_counters", "sqtt", "comm_trace") if x in svc] or ["none"]
     k = 0
     while time.time() < end:
         work()
@@ -79,10 +83,13 @@ def main() -> int:
             work()
             ok = tt.finish(timeout_s=20).get("traced") == 1
             shutil.rmtree(d, ignore_errors=True)
-        else:
+        elif kind == "comm_trace":
             with agent.CommTrace() as ct:
                 work()
             ok = any(o["op"] == "AllGather" for o in ct.summary(last=0)["ops"])
+        else:
+            work()
+            ok = True
         st = ag.stats()
         rounds.append({"kind": kind, "ok": ok, "s": round(time.time() - t0, 3), "rss_mb": round(rss_mb(), 1),
                        "gpu_mb": round(torch.cuda.memory_allocated() / 2**20, 1),
