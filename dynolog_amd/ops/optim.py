@@ -87,6 +87,21 @@ class FusedAdamW(torch.optim.Optimizer):
                                     st["exp_avg_sq"].data_ptr(), p.numel(), 0]
         return arr
 
+    def state_dict(self):
+        """torch.optim.AdamW-compatible: the step count goes out as a 0-d float
+        tensor, as torch stores it (torch's AdamW refuses plain ints).  The
+        live state keeps a Python int (no per-step tensor per parameter); the
+        packed per-param dicts are copies, so the live state is untouched."""
+        sd = super().state_dict()
+        packed = {}
+        for k, st in sd["state"].items():
+            st = dict(st)
+            if "step" in st and not torch.is_tensor(st["step"]):
+                st["step"] = torch.tensor(float(st["step"]))
+            packed[k] = st
+        sd["state"] = packed
+        return sd
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None

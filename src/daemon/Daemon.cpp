@@ -292,6 +292,8 @@ bool Daemon::start(std::string* err) {
       size_t added = 0;
       for (int pid : pids) {
         const std::string path = tracing::kinetoTracePath(log, pid);
+        // read and rewrite the trace as its owner would (the daemon may be root)
+        tracing::ScopedFsIdentity asOwner(pid, path);
         Json trace;
         std::string err;
         // libkineto starts at its next poll / warm-up and writes at the end

@@ -606,7 +606,7 @@ void Agent::samplerLoop() {
   std::string err;
   bool wasPaused = false;
   while (!stopFlag_) {
-    if (paused_) {
+    if (paused_ || samplerHold_) {
       if (staged > 0) {
         if (!flushBatch(staged, &err)) lastError_ = err;
         staged = 0;
@@ -1134,6 +1134,11 @@ void Agent::setSampleHz(double hz) {
 }
 
 void Agent::pause() { paused_ = true; }
+bool Agent::holdSampler() {
+  if (samplerHold_.exchange(true)) return false;
+  usleep(5000);  // the sampler loop stops its counting context within ~2 ms
+  return true;
+}
 void Agent::resume() { paused_ = false; }
 
 // Control channel to the node daemon: periodic "gctx" registration and
@@ -1249,7 +1254,7 @@ void Agent::controlLoop() {
 }
 
 // "sqtt" over the control channel: capture the next N matching dispatches
-// of this process (ThreadTracer), with the counter sampler paused, and
+// of this process (ThreadTracer), with the counter sampler held, and
 // answer with a compact summary (the full index stays in its file: a
 // datagram cannot carry long symbol lists).
 Json Agent::sqttRequest(const Json& req, Json res) {
@@ -1260,11 +1265,9 @@ Json Agent::sqttRequest(const Json& req, Json res) {
   r.outDir = req.contains("out_dir") && req.at("out_dir").isString() ? req.at("out_dir").asString() : "";
   r.agentIndex = sampler_ ? sampler_->agent().index : -1;
   const int timeoutMs = req.contains("timeout_ms") ? static_cast<int>(req.at("timeout_ms").asInt()) : 10000;
-  const bool pauseHere = !paused_;
-  if (pauseHere) {
-    pause();
-    usleep(5000);  // the sampler loop stops its counting context within ~2 ms
-  }
+  // hold the sampler only: pause() would also skip this rank's gathers in
+  // step() while its peers issue theirs (a collective mismatch at world > 1)
+  const bool holdHere = holdSampler();
   std::string err;
   if (!tt.start(r, &err)) {
     res["status"] = "failed: " + err;
@@ -1288,12 +1291,12 @@ Json Agent::sqttRequest(const Json& req, Json res) {
       }
     res["dispatches"] = d;
   }
-  if (pauseHere) resume();
+  if (holdHere) releaseSampler();
   return res;
 }
 
 // "dispatch_counters" over the control channel: exact counters of the next N
-// matching dispatches (DispatchCounters), sampler paused; the reply carries
+// matching dispatches (DispatchCounters), sampler held; the reply carries
 // the per-kernel averages and at most 16 dispatches (datagram size).
 Json Agent::dispatchCountersRequest(const Json& req, Json res) {
   auto& dc = DispatchCounters::get();
@@ -1303,11 +1306,9 @@ Json Agent::dispatchCountersRequest(const Json& req, Json res) {
   r.counterSet = req.contains("counter_set") && req.at("counter_set").isString() ? req.at("counter_set").asString() : "lite";
   r.agentIndex = sampler_ ? sampler_->agent().index : -1;
   const int timeoutMs = req.contains("timeout_ms") ? static_cast<int>(req.at("timeout_ms").asInt()) : 10000;
-  const bool pauseHere = !paused_;
-  if (pauseHere) {
-    pause();
-    usleep(5000);  // the sampler loop stops its counting context within ~2 ms
-  }
+  // hold the sampler only: pause() would also skip this rank's gathers in
+  // step() while its peers issue theirs (a collective mismatch at world > 1)
+  const bool holdHere = holdSampler();
   std::string err;
   if (!dc.start(r, &err)) {
     res["status"] = "failed: " + err;
@@ -1327,7 +1328,7 @@ Json Agent::dispatchCountersRequest(const Json& req, Json res) {
       }
     res["dispatches"] = d;
   }
-  if (pauseHere) resume();
+  if (holdHere) releaseSampler();
   return res;
 }
 
@@ -1604,6 +1605,8 @@ void Agent::releaseDevice() {
 Json Agent::stats() const {
   Json j = Json::object();
   j["running"] = running_.load();
+  j["paused"] = paused_.load();
+  j["sampler_held"] = samplerHold_.load();
   j["rank"] = cfg_.jobRank();
   j["world"] = cfg_.jobWorld > 0 ? cfg_.jobWorld : cfg_.world;
   // the gather group (= the job unless gather_scope "node" split a multi-node job)

@@ -123,6 +123,12 @@ class Agent {
   void stop();
   bool running() const { return running_; }
   bool paused() const { return paused_; }
+  // Stop only the sampler thread for an on-demand capture that programs the
+  // SQ itself (SQTT, dispatch counting); step() keeps gathering, so the
+  // ranks' collectives stay matched.  False if the sampler was already held.
+  bool holdSampler();
+  void releaseSampler() { samplerHold_ = false; }
+  bool samplerHeld() const { return samplerHold_; }
 
   Json stats() const;
   // Slots per rank whose sample time lies in [t0, t1] (CLOCK_MONOTONIC ns).
@@ -167,6 +173,10 @@ class Agent {
   std::atomic<bool> running_{false};
   std::atomic<bool> stopFlag_{false};
   std::atomic<bool> paused_{false};
+  // Holds only the sampler thread (on-demand captures from the control
+  // thread); unlike paused_ it never gates step(), so a rank in a collective
+  // gather keeps issuing its gathers while it is being captured.
+  std::atomic<bool> samplerHold_{false};
   std::atomic<bool> resetPrev_{false};
   std::atomic<bool> gatherFailed_{false};
   std::atomic<uint64_t> flushReq_{0}, flushAck_{0};

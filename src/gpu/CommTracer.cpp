@@ -33,6 +33,15 @@ uint64_t ptr(A p) {
   return reinterpret_cast<uint64_t>(p);
 }
 
+// A communicator's size as RCCL knows it (the library that created the
+// communicator is loaded in this process); 0 when it cannot be asked
+int rcclCommCount(void* comm) {
+  using CountFn = int (*)(void*, int*);
+  static auto count = reinterpret_cast<CountFn>(dlsym(RTLD_DEFAULT, "ncclCommCount"));
+  int n = 0;
+  return comm && count && count(comm, &n) == 0 ? n : 0;
+}
+
 // comm registry: sizes of communicators as they are created
 void registryCb(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
   if (rec.kind != ROCPROFILER_CALLBACK_TRACING_RCCL_API || rec.phase != ROCPROFILER_CALLBACK_PHASE_EXIT) return;
@@ -50,12 +59,9 @@ void registryCb(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data
       break;
     case ROCPROFILER_RCCL_API_ID_ncclCommSplit:
       if (a.ncclCommSplit.newcomm && *a.ncclCommSplit.newcomm) {
-        // the split's size is only known to RCCL: ask it (the library that
-        // just returned the communicator is loaded in this process)
-        using CountFn = int (*)(void*, int*);
-        static auto count = reinterpret_cast<CountFn>(dlsym(RTLD_DEFAULT, "ncclCommCount"));
-        int n = 0;
-        if (count && count(*a.ncclCommSplit.newcomm, &n) == 0) ct.onCommCreated(ptr(*a.ncclCommSplit.newcomm), n);
+        // the split's size is only known to RCCL: ask it
+        const int n = rcclCommCount(*a.ncclCommSplit.newcomm);
+        if (n > 0) ct.onCommCreated(ptr(*a.ncclCommSplit.newcomm), n);
       }
       break;
     case ROCPROFILER_RCCL_API_ID_ncclCommDestroy:
@@ -114,6 +120,12 @@ void traceCb(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*
   }
   c.op = c.op.substr(4);  // drop "nccl"
   c.nranks = ct.ranksOf(c.comm);
+  if (c.nranks == 0) {
+    // a communicator the registry never saw created (ncclCommInitAll, or one
+    // made before tracing was configured): ask RCCL once and remember it
+    c.nranks = rcclCommCount(reinterpret_cast<void*>(c.comm));
+    if (c.nranks > 0) ct.onCommCreated(c.comm, c.nranks);
+  }
   const uint64_t n = perRank ? static_cast<uint64_t>(std::max(c.nranks, 1)) : 1;
   c.bytes = c.count * CommTracer::dtypeSize(c.dtype) * n;
   ct.onCall(c);
@@ -332,6 +344,8 @@ Json CommTracer::summary(size_t lastCalls) const {
     o["calls"] = static_cast<unsigned long long>(a.calls);
     o["bytes"] = static_cast<unsigned long long>(a.bytes);
     o["avg_bytes"] = a.calls ? static_cast<double>(a.bytes) / a.calls : 0.0;
+    // size unknown: per-rank-count ops are priced for 1 rank and busbw is omitted
+    if (a.nranks <= 0) o["nranks_unknown"] = true;
     o["host_us"] = a.hostUs;
     if (a.gpuCalls) {
       o["gpu_calls"] = static_cast<unsigned long long>(a.gpuCalls);

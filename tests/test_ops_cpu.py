@@ -84,3 +84,30 @@ def test_activation_transpose_slot_offer_take():
     ops.offer_transposed(y, y.t().contiguous())
     assert ops._ACT_T[0][0][0] == y.data_ptr()  # one slot: the newest offer
     assert ops.take_transposed(y) is not None and ops._ACT_T[0] is None
+
+
+def test_fused_adamw_state_dict_loads_into_torch_adamw():
+    """FusedAdamW.state_dict() -> torch.optim.AdamW.load_state_dict() -> step():
+    the step count goes out as torch stores it (a tensor), while FusedAdamW's
+    own state keeps its int; and a torch state dict loads back."""
+    import torch
+    from dynolog_amd.ops.optim import FusedAdamW
+
+    p = torch.nn.Parameter(torch.randn(4, 3))
+    opt = FusedAdamW([p], lr=1e-2)
+    st = opt.state[p]
+    st["step"] = 3  # as FusedAdamW.step() leaves it
+    st["exp_avg"] = torch.full_like(p, 0.1)
+    st["exp_avg_sq"] = torch.full_like(p, 0.01)
+    sd = opt.state_dict()
+    assert torch.is_tensor(sd["state"][0]["step"]) and float(sd["state"][0]["step"]) == 3.0
+    assert opt.state[p]["step"] == 3 and isinstance(opt.state[p]["step"], int)  # live state untouched
+    q = torch.nn.Parameter(p.detach().clone())
+    ref = torch.optim.AdamW([q], lr=1e-2)
+    ref.load_state_dict(sd)
+    q.grad = torch.ones_like(q)
+    ref.step()  # raised 'state_steps ... singleton tensors' with an int step
+    assert float(ref.state[q]["step"]) == 4.0
+    back = FusedAdamW([torch.nn.Parameter(q.detach().clone())], lr=1e-2)
+    back.load_state_dict(ref.state_dict())
+    assert float(back.state_dict()["state"][0]["step"]) == 4.0
