@@ -54,7 +54,7 @@ STAGE_META_DTYPE = np.dtype([("host_ts_ns", "<u8"), ("latency_ns", "<u4"), ("n_r
 
 GATHER_HEADER_DTYPE = np.dtype([
     ("first_seq", "<u8"), ("count", "<u4"), ("rank", "<u4"), ("dropped", "<u8"),
-    ("head", "<u8"), ("backlog", "<u8"), ("cap", "<u4"), ("device", "<i4"), ("reserved", "<u8", (2,)),
+    ("head", "<u8"), ("backlog", "<u8"), ("cap", "<u4"), ("device", "<i4"), ("pci_loc", "<u8"), ("reserved", "<u8"),
 ])
 assert GATHER_HEADER_DTYPE.itemsize == 64
 

@@ -82,11 +82,17 @@ struct AgentConfig {
   bool daemonControl = false;        // register with the daemon, serve kernel-trace requests
                                      // (default: on when the "daemon" sink is used)
   uint64_t faultGatherAtStep = 0;    // fault injection ("gather_error@N"), 0 = off
+  bool faultSkipCommInit = false;    // fault injection ("skip_comm_init"): this rank never
+                                     // joins the agent communicator (its peers must time out)
+  int commInitTimeoutMs = 60000;     // deadline for every rank to join the communicator
   std::string slotRing;              // rank 0: publish every received slot into this shm ring
   uint64_t slotRingBytes = 64ull << 20;  // (256k slots = ~4 min of 1 kHz x 1 GPU)
 
   static AgentConfig fromJson(const Json& j);
 };
+
+// "dddd:bb:dd.f" of a rocprofiler agent (pciLocString: SlotAggregator.h)
+std::string agentBdf(const AgentInfo& a);
 
 class Agent {
  public:
@@ -177,6 +183,10 @@ class Agent {
   // thread); unlike paused_ it never gates step(), so a rank in a collective
   // gather keeps issuing its gathers while it is being captured.
   std::atomic<bool> samplerHold_{false};
+  uint64_t pciLoc_ = 0;  // this rank's GPU (DynoGatherHeader::pci_loc)
+  // The agent's communicator is non-blocking (init can be abandoned at a
+  // deadline): wait for a call that returned ncclInProgress to finish.
+  int ncclSettle(int result, uint64_t timeoutNs);
   std::atomic<bool> resetPrev_{false};
   std::atomic<bool> gatherFailed_{false};
   std::atomic<uint64_t> flushReq_{0}, flushAck_{0};

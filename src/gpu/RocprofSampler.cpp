@@ -100,6 +100,13 @@ std::vector<std::string> counterNamesForSet(const std::string& set, std::string*
   return out;
 }
 
+unsigned selectedCounterMask(const std::vector<std::string>& names) {
+  unsigned m = 0;
+  for (size_t i = 0; i < names.size() && i < 32; ++i)
+    if (!names[i].empty()) m |= 1u << i;
+  return m;
+}
+
 std::vector<CounterPassSpec> parseCounterPasses(const std::string& spec, const std::string& defaultSet,
                                                 std::string* err) {
   std::vector<CounterPassSpec> out;

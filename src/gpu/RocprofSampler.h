@@ -162,6 +162,9 @@ struct CounterPassSpec {
 // "" -> a single pass of defaultSet.  Sets: full | lite | lean | core (main
 // pass), precision (per-precision VALU FLOPs, MFMA MOPs by type, VALU busy,
 // plus TCC + GRBM), or a '+'-joined list of main-pass counter names.
+// delta[] positions a pass selected (non-empty names), as a bit mask
+unsigned selectedCounterMask(const std::vector<std::string>& names);
+
 std::vector<CounterPassSpec> parseCounterPasses(const std::string& spec, const std::string& defaultSet,
                                                 std::string* err);
 

@@ -145,8 +145,15 @@ typedef struct DynoGatherHeader {
   uint64_t backlog;    // pending slots this rank keeps for its next gathers
   uint32_t cap;        // payload capacity of this gather (slots per rank)
   int32_t device;      // HIP device index of this rank's GPU
-  uint64_t reserved[2];
+  uint64_t pci_loc;    // PCI location of that GPU: domain << 16 | bus << 8 | dev << 3 | fn (0 = unknown)
+  uint64_t reserved;
 } DynoGatherHeader;
+
+// PCI location <-> "dddd:bb:dd.f" (the key the daemon matches GPUs on: HIP
+// device indices differ between processes under *_VISIBLE_DEVICES)
+static inline uint64_t dynoPciLoc(uint32_t domain, uint32_t bus, uint32_t dev, uint32_t fn) {
+  return ((uint64_t)domain << 16) | ((uint64_t)(bus & 0xff) << 8) | ((uint64_t)(dev & 0x1f) << 3) | (fn & 7);
+}
 
 // Layout entry for one raw record index: which counter it belongs to.
 typedef struct DynoLayout {

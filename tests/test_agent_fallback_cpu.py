@@ -112,7 +112,7 @@ def test_rccl_then_shm_failure_ends_on_local_sampling():
     out = _run(2, (1,), local_world=2, fail_modes=("gather", "shm"))
     for rank, (mode, frm, reason, calls) in out.items():
         assert mode == "none" and frm == "gather", out
-        assert reason.startswith("ncclCommInitRank") and "then shm gather" in reason, reason
+        assert reason.startswith("rank 1: ncclCommInitRank") and "then rank 1: shm gather" in reason, reason
         assert [c[1] for c in calls if c[0] == "start"] == ["gather", "shm", "none"], calls
 
 
@@ -269,3 +269,25 @@ def test_preinit_uses_tool_discovery_under_kineto_daemon_mode(native_built):
                           os.path.join(repo, "dynolog_amd", "lib", "libdyno_gpu.so")],
                          capture_output=True, text=True).stdout
     assert " rocprofiler_configure" not in out
+
+
+def test_fallback_reason_names_every_failing_rank():
+    out = _run(2, (0, 1), local_world=2)
+    for rank, (mode, frm, reason, calls) in out.items():
+        assert "rank 0: ncclCommInitRank" in reason and "rank 1: ncclCommInitRank" in reason, reason
+
+
+def test_bench_fault_spec_targets_one_rank():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.fault_for_rank("skip_comm_init@1", 1) == "skip_comm_init"
+    assert bench.fault_for_rank("skip_comm_init@1", 0) == ""
+    assert bench.fault_for_rank("gather_error@5@0", 0) == "gather_error@5"
+    assert bench.fault_for_rank("", 3) == ""
+    with pytest.raises(SystemExit):
+        bench.fault_for_rank("skip_comm_init", 0)
+    a = bench.parse_args(["--gpus", "2"])
+    assert a.comm_trace == "auto" and a.comm_init_timeout_s == 60.0

@@ -206,6 +206,7 @@ def test_gather_prep(native_built, ring, written, cursor, cap):
     assert hdr["dropped"] == dropped
     assert hdr["backlog"] == backlog
     assert hdr["cap"] == cap and hdr["device"] == 3
+    assert hdr["pci_loc"] == 0x7500  # 0000:75:00.0, passed through
     assert hdr["head"] == written
     assert hdr["rank"] == 5
     assert need.value == written - cursor
