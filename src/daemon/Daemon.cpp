@@ -346,6 +346,7 @@ bool Daemon::start(std::string* err) {
     // GPU agents inside training processes may forward their per-GPU
     // counter records to the daemon ("gmet" messages).
     ipc_->setMetricsCallback([this](const Json& rec) {
+      noteAgentGpuRecord(rec, static_cast<uint64_t>(nowNsMonotonic() / 1000000));
       auto l = makeLogger("gpu_counters");
       if (rec.isObject()) {
         for (const auto& [k, v] : rec.asObject()) {

@@ -10,6 +10,7 @@
 
 #include "common/Logging.h"
 #include "common/System.h"
+#include "gpu/CountableMark.h"
 #include "gpu/KernelTracer.h"
 #include "gpu/CommTracer.h"
 #include "gpu/DispatchCounters.h"
@@ -74,6 +75,13 @@ std::vector<std::string> counterNamesForSet(const std::string& set, std::string*
     // cost is mostly per SQ instance (profiles/round2/g18), so keep 2 of 8
     disable({DC_SQ_WAVES, DC_SQ_BUSY_CYCLES, DC_SQ_WAVE_CYCLES, DC_SQ_INSTS_LDS, DC_SQ_LDS_BANK_CONFLICT,
              DC_SQ_LDS_IDX_ACTIVE, DC_TCC_EA0_WRREQ_64B, DC_TCC_EA0_RDREQ_32B});
+    return names;
+  }
+  if (set == "xproc") {
+    // the counters the daemon can read for any process (CounterVisibility.h):
+    // MFMA busy + bf16 MOPs and the GRBM clocks
+    disable({DC_SQ_WAVES, DC_SQ_BUSY_CYCLES, DC_SQ_WAVE_CYCLES, DC_SQ_INSTS_LDS, DC_SQ_LDS_BANK_CONFLICT,
+             DC_SQ_LDS_IDX_ACTIVE, DC_TCC_EA0_RDREQ, DC_TCC_EA0_WRREQ, DC_TCC_EA0_WRREQ_64B, DC_TCC_EA0_RDREQ_32B});
     return names;
   }
   if (set == "core") {
@@ -292,6 +300,7 @@ int RocprofRuntime::toolInit() {
     ai.local_mem_bytes = a.local_mem_size;
     agents_.push_back(ai);
   }
+  std::vector<uint64_t> countableGpus;
   for (const auto& ai : agents_) {
     if (!wantDevices_.empty() &&
         std::find(wantDevices_.begin(), wantDevices_.end(), ai.index) == wantDevices_.end())
@@ -328,7 +337,10 @@ int RocprofRuntime::toolInit() {
       continue;
     }
     ctxs_[ai.index] = std::move(c);
+    countableGpus.push_back(ai.gpu_id);
   }
+  // the daemon counts this process's waves on these GPUs (CountableMark.h)
+  dynoMarkCountable(countableGpus);
   if (kernelTrace_) {
     auto& kt = KernelTracer::get();
     for (const auto& ai : agents_) kt.setAgentIndex(ai.handle, ai.index);

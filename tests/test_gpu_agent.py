@@ -407,6 +407,8 @@ def test_lean_counter_set_keeps_mfma_and_hbm(native_built):
                                    "TCC_EA0_RDREQ", "TCC_EA0_WRREQ", "GRBM_GUI_ACTIVE", "GRBM_COUNT"}
     assert last["mfma_util"] > 5.0 and last["mfma_bf16_tflops"] > 50.0, last
     assert last["hbm_read_gbps"] > 0.0, last
+    # the SQ wave counters were not selected: no 0-valued occupancy / waves
+    assert "occupancy_pct" not in last and "waves_per_us" not in last and "SQ_WAVES" not in last, last
 
 
 def test_kernel_counters_demix_gemm_and_copy(native_built):
