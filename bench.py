@@ -108,6 +108,14 @@ def parse_args(argv=None):
                    help="time the workload in child processes that never load the agent (no "
                         "rocprofiler tool, no buffers): one before this run and one after it, the "
                         "baseline BASELINE.md defines -> overhead_vs_no_agent_pct (auto = on with the agent)")
+    p.add_argument("--overhead-matrix", default="",
+                   help="instead of the headline: price sampling per counter set, e.g. "
+                        "'core,lean,lite,full,core:3/lite:1' (an entry with ':' is a pass plan, '/' between "
+                        "passes): pooled A/B overhead and overhead against no-agent children for each, at "
+                        "--sample-hz, plus a no-agent child with only libdyno_countable.so loaded; fit "
+                        "overhead = a + b * instances * rate -> --matrix-out (JSON)")
+    p.add_argument("--matrix-out", default="", help="JSON file of --overhead-matrix")
+    p.add_argument("--countable-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--baseline-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
@@ -125,7 +133,7 @@ def baseline_child_env(environ) -> dict:
     return env
 
 
-def run_baseline_child(args, tag: str) -> dict:
+def run_baseline_child(args, tag: str, countable: bool = False) -> dict:
     """Times the same workload (model, batch, sequence, optimizer, steps) in a
     child process that never loads the agent: no rocprofiler-sdk tool is
     registered, no agent buffers exist.  Under torchrun every rank starts its
@@ -141,11 +149,16 @@ def run_baseline_child(args, tag: str) -> dict:
            "--optimizer", args.optimizer, "--batches", str(args.batches), "--host-pmu", "off",
            "--no-agent-baseline", "off", "--json-out", path]
     env = baseline_child_env(os.environ)
+    env.pop("ROCP_TOOL_LIBRARIES", None)
+    if countable:
+        # the job-side opt-in alone: a counting context configured, never started
+        from dynolog_amd import _native
+        env["ROCP_TOOL_LIBRARIES"] = _native.COUNTABLE_LIB
     t0 = time.time()
     try:
         # the child's stdout goes to stderr: rank 0's stdout carries ONE result line
         r = subprocess.run(cmd, env=env, stdout=sys.stderr, timeout=600)
-        res = {"tag": tag, "rc": r.returncode, "wall_s": round(time.time() - t0, 1)}
+        res = {"tag": tag, "rc": r.returncode, "wall_s": round(time.time() - t0, 1), "countable": countable}
         if r.returncode == 0 and os.path.getsize(path) > 0:
             with open(path) as f:
                 res["ms_per_step"] = json.loads(f.read())["ms_per_step"]
@@ -199,6 +212,38 @@ def relaunch_under_torchrun(args, argv) -> int:
         return 124
 
 
+def matrix_entries(spec: str):
+    """'core,lean,core:3/lite:1' -> [(label, counter_set, counter_passes)]."""
+    out = []
+    for item in [x.strip() for x in spec.split(",") if x.strip()]:
+        if ":" in item:
+            out.append((item, "lite", item.replace("/", ",")))
+        else:
+            out.append((item, item, ""))
+    return out
+
+
+def fit_overhead(points):
+    """Least squares of overhead % = a + b * x over (x, overhead) points,
+    x = raw instances x samples/s (the work the command processor does per
+    second on the agent's behalf).  Returns a, b (per 1e6 instance reads / s), r2."""
+    pts = [(x, y) for x, y in points if x is not None and y is not None]
+    if len(pts) < 2:
+        return None
+    n = len(pts)
+    mx = sum(x for x, _ in pts) / n
+    my = sum(y for _, y in pts) / n
+    sxx = sum((x - mx) ** 2 for x, _ in pts)
+    if sxx <= 0:
+        return None
+    b = sum((x - mx) * (y - my) for x, y in pts) / sxx
+    a = my - b * mx
+    ss = sum((y - my) ** 2 for _, y in pts)
+    res = sum((y - (a + b * x)) ** 2 for x, y in pts)
+    return {"a_pct": round(a, 4), "b_pct_per_M_reads_per_s": round(b * 1e6, 4),
+            "r2": round(1.0 - res / ss, 3) if ss > 0 else None, "points": n}
+
+
 def fault_for_rank(spec: str, rank: int) -> str:
     """--agent-fault-inject SPEC@RANK -> SPEC on that rank, "" elsewhere
     (SPEC itself may contain '@', e.g. gather_error@5@0)."""
@@ -208,6 +253,105 @@ def fault_for_rank(spec: str, rank: int) -> str:
     if not body or not who.isdigit():
         raise SystemExit(f"--agent-fault-inject: expected SPEC@RANK, got {spec!r}")
     return body if int(who) == rank else ""
+
+
+def run_overhead_matrix(args, ag, env, train_step, timed, no_agent_runs):
+    """--overhead-matrix: for each counter set (or pass plan), restart the
+    agent with it, then price it with --ab-rounds interleaved sampling /
+    paused windows of --ab-steps (pooled, as the headline) and against the
+    no-agent children timed before this process touched the GPU (and, after
+    the sets, once more, plus a child with only libdyno_countable.so)."""
+    import torch
+    from dynolog_amd import agent as dagent
+    rows = []
+    entries = matrix_entries(args.overhead_matrix)
+    for label, cset, passes in entries:
+        if rows or (cset, passes) != (args.counter_set, args.counter_passes):  # else: main()'s agent
+            ag.stop()
+            ag = dagent.GpuAgent.start(device=ag.config.get("device", 0), rank=env.rank, world=env.world,
+                                       sample_hz=args.sample_hz, batch=args.pack_batch,
+                                       gather_mode=args.gather_mode, log_file=args.log_file,
+                                       counter_set=cset, counter_passes=passes, sinks=("memory",),
+                                       comm_init_timeout_ms=int(args.comm_init_timeout_s * 1000))
+        ag.resume()
+        for _ in range(3):
+            train_step()
+        torch.cuda.synchronize()
+        st0 = ag.stats()
+        t_start = time.perf_counter()
+        active_s = paused_s = 0.0
+        active_n = paused_n = 0
+        for r in range(args.ab_rounds):
+            for want_active in ((True, False) if r % 2 == 0 else (False, True)):
+                if want_active:
+                    ag.resume()
+                    train_step()
+                    torch.cuda.synchronize()
+                    s_, _, _ = timed(args.ab_steps)
+                    active_s, active_n = active_s + s_, active_n + args.ab_steps
+                    ag.pause()
+                    time.sleep(0.02)
+                else:
+                    s_, _, _ = timed(args.ab_steps)
+                    paused_s, paused_n = paused_s + s_, paused_n + args.ab_steps
+        ag.resume()
+        st1 = ag.stats()
+        active_ms = active_s / active_n * 1e3
+        paused_ms = paused_s / paused_n * 1e3
+        taken = st1["samples_taken"] - st0["samples_taken"]
+        row = {"entry": label, "counter_set": cset, "counter_passes": passes or None,
+               "raw_instances": st1.get("raw_instances"),
+               "pass_instances": [p.get("raw_instances") for p in st1.get("counter_passes", [])],
+               "active_ms_per_step": round(active_ms, 3), "paused_ms_per_step": round(paused_ms, 3),
+               "pooled_overhead_pct": round((active_ms / paused_ms - 1.0) * 100.0, 3),
+               # samples over the sampling windows only (the agent is paused in the rest)
+               "samples_per_sec": round(taken / max(active_s, 1e-9), 1),
+               "sample_latency_us_avg": round(st1.get("sample_latency_us_avg", 0.0), 1),
+               "samples_failed": st1.get("samples_failed", 0) - st0.get("samples_failed", 0),
+               "wall_s": round(time.perf_counter() - t_start, 1)}
+        rows.append(row)
+        if env.rank == 0:
+            print("matrix", json.dumps(row), file=sys.stderr, flush=True)
+    ag.pause()
+    want_children = args.no_agent_baseline != "off"
+    if want_children:
+        # free this process's GPU memory, then the after-children: plain, countable-only
+        import gc
+        ag.stop()
+        ag = None
+        torch.cuda.synchronize()
+        gc.collect()
+        torch.cuda.empty_cache()
+        no_agent_runs.append(run_baseline_child(args, "after"))
+        no_agent_runs.append(run_baseline_child(args, "countable", countable=True))
+    plain = [r["ms_per_step"] for r in no_agent_runs if "ms_per_step" in r and not r.get("countable")]
+    countable = [r["ms_per_step"] for r in no_agent_runs if "ms_per_step" in r and r.get("countable")]
+    no_agent_ms = sum(plain) / len(plain) if plain else None
+    pts = []
+    for row in rows:
+        if no_agent_ms:
+            row["overhead_vs_no_agent_pct"] = round((row["active_ms_per_step"] / no_agent_ms - 1.0) * 100.0, 3)
+            row["paused_vs_no_agent_pct"] = round((row["paused_ms_per_step"] / no_agent_ms - 1.0) * 100.0, 3)
+        x = (row["raw_instances"] or 0) * row["samples_per_sec"]
+        row["instance_reads_per_s"] = round(x, 1)
+        pts.append((x, row["pooled_overhead_pct"]))
+    out = {"mode": "overhead_matrix", "model": args.model, "micro_batch": args.micro_batch, "seq_len": args.seq_len,
+           "sample_hz_target": args.sample_hz, "ab_rounds": args.ab_rounds, "ab_steps": args.ab_steps,
+           "rows": rows, "no_agent_runs": no_agent_runs,
+           "no_agent_ms_per_step": round(no_agent_ms, 3) if no_agent_ms else None,
+           "countable_only_ms_per_step": round(countable[0], 3) if countable else None,
+           "countable_only_vs_no_agent_pct": (round((countable[0] / no_agent_ms - 1.0) * 100.0, 3)
+                                              if countable and no_agent_ms else None),
+           "fit_pooled": fit_overhead(pts),
+           "fit_vs_no_agent": fit_overhead([(r["instance_reads_per_s"], r.get("overhead_vs_no_agent_pct"))
+                                            for r in rows])}
+    if env.rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.matrix_out:
+            with open(args.matrix_out, "w") as f:
+                f.write(json.dumps(out, indent=1) + "\n")
+    return ag
 
 
 def main(argv=None) -> int:
@@ -349,6 +493,10 @@ def main(argv=None) -> int:
         for _ in range(args.warmup):
             train_step()
         torch.cuda.synchronize()
+
+        if args.overhead_matrix and ag is not None:
+            ag = run_overhead_matrix(args, ag, env, train_step, timed, no_agent_runs)
+            return 0
 
         base_s = None
         pooled_active_s = None

@@ -1,5 +1,7 @@
 #include "gpu/Agent.h"
 
+#include <malloc.h>
+
 #include <poll.h>
 #include <rccl/rccl.h>
 #include <time.h>
@@ -1668,6 +1670,19 @@ Json Agent::stats() const {
   Json j = Json::object();
   j["running"] = running_.load();
   j["paused"] = paused_.load();
+  // host memory of the process (on-demand services: profiles/round4 soaks)
+  {
+    long rssPages = 0;
+    if (FILE* f = fopen("/proc/self/statm", "r")) {
+      long size = 0;
+      if (fscanf(f, "%ld %ld", &size, &rssPages) != 2) rssPages = 0;
+      fclose(f);
+    }
+    j["host_rss_mb"] = static_cast<double>(rssPages) * static_cast<double>(sysconf(_SC_PAGESIZE)) / (1 << 20);
+    const struct mallinfo2 mi = mallinfo2();
+    j["heap_in_use_mb"] = static_cast<double>(mi.uordblks + mi.hblkhd) / (1 << 20);
+    j["heap_arena_mb"] = static_cast<double>(mi.arena + mi.hblkhd) / (1 << 20);
+  }
   // the GPU this rank's HIP device is, and the GPU its counters are read from
   if (pciLoc_) j["hip_bdf"] = pciLocString(pciLoc_);
   if (sampler_) j["sampled_agent_bdf"] = agentBdf(sampler_->agent());

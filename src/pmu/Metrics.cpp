@@ -29,7 +29,12 @@ std::vector<std::string> Metrics::ids() const {
 std::vector<EventConf> expandEventRef(const PmuDeviceManager& mgr, const EventRef& ref,
                                       std::string* err) {
   std::vector<EventConf> out;
+  // "pmu_*/fields/" or "pmu_*:alias": one event per matching PMU instance
   auto slash = ref.spec.find('/');
+  if (slash == std::string::npos) {
+    const auto colon = ref.spec.find(':');
+    if (colon != std::string::npos && colon > 0 && ref.spec[colon - 1] == '*') slash = colon;
+  }
   std::string pmuName = slash == std::string::npos ? "" : ref.spec.substr(0, slash);
   if (!pmuName.empty() && pmuName.back() == '*') {
     std::string prefix = pmuName.substr(0, pmuName.size() - 1);
@@ -102,10 +107,12 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
         o["ipc"] = ratio(get(c, "instructions"), get(c, "cycles"));
       });
 
-  // --- AMD Zen4/Zen5 core events (AMD PPR event encodings) ---
+  // --- AMD Zen4/Zen5 core events, by their names in the AmdEvents table
+  // (the encodings live in one place; tests check every remaining raw spec
+  // against that table) ---
   std::vector<EventRef> l2 = {{"instructions", "instructions"},
-                              {"l2_miss", "cpu/event=0x64,umask=0x09/"},  // l2_cache_req_stat.ic_dc_miss_in_l2
-                              {"l2_access", "cpu/event=0x64,umask=0xff/"}};
+                              {"l2_miss", "cpu:l2_cache_req_stat.ic_dc_miss_in_l2"},
+                              {"l2_access", "cpu:l2_cache_req_stat.all"}};
   std::vector<EventRef> l2i = {{"instructions", "instructions"},
                                {"l2_miss", "cpu:l2_rqsts.miss"},
                                {"l2_access", "cpu:l2_rqsts.references"}};
@@ -115,8 +122,8 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
         o["l2_hit_rate"] = 1.0 - ratio(get(c, "l2_miss"), get(c, "l2_access"));
       });
   std::vector<EventRef> tlb = {{"instructions", "instructions"},
-                               {"dtlb_miss", "cpu/event=0x45,umask=0xff/"},   // ls_l1_d_tlb_miss.all
-                               {"itlb_miss", "cpu/event=0x85,umask=0x07/"}};  // bp_l1_tlb_miss_l2_tlb_miss
+                               {"dtlb_miss", "cpu:ls_l1_d_tlb_miss.all"},
+                               {"itlb_miss", "cpu:bp_l1_tlb_miss_l2_tlb_miss.all"}};  // all page sizes incl. coalesced 4K
   std::vector<EventRef> tlbi = {{"instructions", "instructions"},
                                 {"dtlb_miss", "cpu:dtlb_load_misses.walk_completed"},
                                 {"itlb_miss", "cpu:itlb_misses.walk_completed"}};
@@ -126,7 +133,7 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
         o["dtlb_mpki"] = ratio(get(c, "dtlb_miss"), get(c, "instructions")) * 1e3;
         o["itlb_mpki"] = ratio(get(c, "itlb_miss"), get(c, "instructions")) * 1e3;
       });
-  std::vector<EventRef> fp = {{"fp_ops", "cpu/event=0x03,umask=0xff/"}};  // fp_ret_sse_avx_ops.all
+  std::vector<EventRef> fp = {{"fp_ops", "cpu:fp_ret_sse_avx_ops.all"}};
   add("fp_ops", "Retired SSE/AVX floating point operations", {{kZen4, fp}, {kZen5, fp}},
       [](const auto& c, double s, double, auto& o) { o["cpu_gflops"] = ratio(get(c, "fp_ops"), s) * 1e-9; });
   add("branches", "Branch misprediction rate",
@@ -136,8 +143,8 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
       });
 
   // --- L3 (amd_l3 uncore, one PMU per CCX; opened on its cpumask) ---
-  std::vector<EventRef> l3 = {{"l3_access", "amd_l3/event=0x04,umask=0xff/"},
-                              {"l3_miss", "amd_l3/event=0x04,umask=0x01/"}};
+  std::vector<EventRef> l3 = {{"l3_access", "amd_l3:l3_lookup_state.all_coherent_accesses_to_l3"},
+                              {"l3_miss", "amd_l3:l3_lookup_state.l3_miss"}};
   add("l3_cache", "L3 lookups, misses and miss ratio (all CCXs)", {{kZen4, l3}, {kZen5, l3}},
       [](const auto& c, double s, double, auto& o) {
         o["l3_miss_ratio"] = ratio(get(c, "l3_miss"), get(c, "l3_access"));
@@ -146,8 +153,8 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
       true);
 
   // --- DRAM bandwidth: Zen5 UMC CAS commands x 64 B, summed over amd_umc_* ---
-  std::vector<EventRef> umc = {{"dram_rd_bytes", "amd_umc_*/event=0x0a,rdwrmask=0x1/", 64.0},
-                               {"dram_wr_bytes", "amd_umc_*/event=0x0a,rdwrmask=0x2/", 64.0}};
+  std::vector<EventRef> umc = {{"dram_rd_bytes", "amd_umc_*:umc_cas_cmd.rd", 64.0},
+                               {"dram_wr_bytes", "amd_umc_*:umc_cas_cmd.wr", 64.0}};
   // --- Zen4: data-fabric read/write data beats x 64 B, 12 channels per
   // package (amd_df, one PMU per package; 24 events split into groups of 4
   // that the kernel multiplexes).  Reference: AmdEvents.h:58-79 DFPmuMsrAmd,
@@ -155,13 +162,13 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
   auto df = [](bool rd, bool wr, const char* rdNick, const char* wrNick, double scale) {
     std::vector<EventRef> v;
     for (int ch = 0; ch < kZen4DramChannels; ++ch) {
-      char spec[64];
+      char spec[96];
       if (rd) {
-        snprintf(spec, sizeof(spec), "amd_df/event=0x%x,umask=0x7fe/", zen4DfDramEventCode(ch));
+        snprintf(spec, sizeof(spec), "amd_df:local_or_remote_socket_read_data_beats_dram_%d", ch);
         v.push_back({rdNick, spec, scale});
       }
       if (wr) {
-        snprintf(spec, sizeof(spec), "amd_df/event=0x%x,umask=0x7ff/", zen4DfDramEventCode(ch));
+        snprintf(spec, sizeof(spec), "amd_df:local_or_remote_socket_write_data_beats_dram_%d", ch);
         v.push_back({wrNick, spec, scale});
       }
     }
@@ -217,7 +224,7 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
         o["l3_mpki"] = ratio(get(c, "l3_miss"), get(c, "instructions")) * 1e3;
       },
       true);
-  std::vector<EventRef> dramRd = {{"cas_rd", "amd_umc_*/event=0x0a,rdwrmask=0x1/"}};
+  std::vector<EventRef> dramRd = {{"cas_rd", "amd_umc_*:umc_cas_cmd.rd"}};
   add("dram_access_reads", "DRAM 64-B reads and bytes (Zen5: all UMCs; Zen4: DF read beats, all channels)",
       {{kZen5, dramRd}, {kZen4, df(true, false, "cas_rd", "", 1.0)}},
       [](const auto& c, double s, double, auto& o) {

@@ -291,3 +291,18 @@ def test_bench_fault_spec_targets_one_rank():
         bench.fault_for_rank("skip_comm_init", 0)
     a = bench.parse_args(["--gpus", "2"])
     assert a.comm_trace == "auto" and a.comm_init_timeout_s == 60.0
+
+
+def test_bench_overhead_matrix_helpers():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod2", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.matrix_entries("core, lean,core:3/lite:1") == [
+        ("core", "core", ""), ("lean", "lean", ""), ("core:3/lite:1", "lite", "core:3,lite:1")]
+    # overhead = 0.1 % + 0.5 % per million instance reads / s
+    pts = [(x, 0.1 + 0.5e-6 * x) for x in (272e3, 336e3, 528e3, 784e3)]
+    f = bench.fit_overhead(pts)
+    assert abs(f["a_pct"] - 0.1) < 1e-6 and abs(f["b_pct_per_M_reads_per_s"] - 0.5) < 1e-6 and f["r2"] == 1.0
+    assert bench.fit_overhead([(1.0, 2.0)]) is None
