@@ -578,6 +578,15 @@ def main(argv=None) -> int:
                 base_s = paused_s / paused_n * args.steps
                 pooled_active_s = active_s / active_n * args.steps
 
+        collectives = None
+        if use_agent and comm_trace:
+            # one more step, outside every timed window, with its RCCL calls traced
+            # (before the after-child frees the model)
+            ct = dagent.CommTrace().start()
+            train_step()
+            torch.cuda.synchronize()
+            ct.stop()
+            collectives = ct.summary(last=0)
         if want_no_agent and not args.sweep_hz:
             # the second no-agent run, after this one: free this process's
             # workload memory and stop sampling while the child runs
@@ -596,14 +605,6 @@ def main(argv=None) -> int:
         window_s = (m1 - m0) * 1e-9 if ag is not None else meas_s
         value = total_samples / window_s if window_s > 0 else 0.0
         tokens = B * S * env.world * args.steps
-        collectives = None
-        if use_agent and comm_trace:
-            # one more step, outside every timed window, with its RCCL calls traced
-            ct = dagent.CommTrace().start()
-            train_step()
-            torch.cuda.synchronize()
-            ct.stop()
-            collectives = ct.summary(last=0)
         out = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -78,6 +78,14 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
   auto add = [&](std::string id, std::string desc,
                  std::map<std::optional<CpuArch>, std::vector<EventRef>> ev, DeriveFn f,
                  bool sysOnly = false) {
+    // Emerald / Granite Rapids take SPR's events (same core encodings);
+    // Haswell-EP / Broadwell-EP the Skylake-SP names their table defines
+    if (ev.count(kSpr))
+      for (CpuArch a : {CpuArch::IntelEmeraldRapids, CpuArch::IntelGraniteRapids})
+        if (!ev.count(a)) ev[a] = ev.at(kSpr);
+    if (ev.count(kSkx) && (id == "l2_cache_misses" || id == "tlb_misses" || id == "l3_cache_misses_per_instruction"))
+      for (CpuArch a : {CpuArch::IntelHaswellX, CpuArch::IntelBroadwellX})
+        if (!ev.count(a)) ev[a] = ev.at(kSkx);
     auto m = std::make_shared<MetricDesc>();
     m->id = std::move(id);
     m->description = std::move(desc);
@@ -293,11 +301,16 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
                                  {"flops", b + "256b_packed_" + prec, 4.0 * w}, {"flops", b + "512b_packed_" + prec, 8.0 * w}};
   };
   const auto fpSingle = fpPrec("single", 2.0), fpDouble = fpPrec("double", 1.0);
+  auto no512 = [](std::vector<EventRef> v) {  // Broadwell: no 512-bit forms
+    v.erase(std::remove_if(v.begin(), v.end(), [](const EventRef& r) { return r.spec.find("512b") != std::string::npos; }),
+            v.end());
+    return v;
+  };
   add("fp_instrs_single_precision", "Single-precision FP FLOPs retired (scalar + packed, by vector width)",
-      {{kSkx, fpSingle}, {kIcx, fpSingle}, {kSpr, fpSingle}},
+      {{kSkx, fpSingle}, {kIcx, fpSingle}, {kSpr, fpSingle}, {CpuArch::IntelBroadwellX, no512(fpSingle)}},
       [](const auto& c, double s, double, auto& o) { o["fp_single_gflops"] = ratio(get(c, "flops"), s) * 1e-9; });
   add("fp_instrs_double_precision", "Double-precision FP FLOPs retired (scalar + packed, by vector width)",
-      {{kSkx, fpDouble}, {kIcx, fpDouble}, {kSpr, fpDouble}},
+      {{kSkx, fpDouble}, {kIcx, fpDouble}, {kSpr, fpDouble}, {CpuArch::IntelBroadwellX, no512(fpDouble)}},
       [](const auto& c, double s, double, auto& o) { o["fp_double_gflops"] = ratio(get(c, "flops"), s) * 1e-9; });
   std::vector<EventRef> br = {{"brn", "cpu:ex_ret_brn"},
                               {"brn_misp", "cpu:ex_ret_brn_misp"},

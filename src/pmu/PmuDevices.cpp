@@ -21,6 +21,10 @@ const char* cpuArchName(CpuArch a) {
     case CpuArch::IntelSkylakeX: return "intel_skx";
     case CpuArch::IntelIceLakeX: return "intel_icx";
     case CpuArch::IntelSapphireRapids: return "intel_spr";
+    case CpuArch::IntelEmeraldRapids: return "intel_emr";
+    case CpuArch::IntelGraniteRapids: return "intel_gnr";
+    case CpuArch::IntelHaswellX: return "intel_hsx";
+    case CpuArch::IntelBroadwellX: return "intel_bdx";
     default: return "unknown";
   }
 }
@@ -29,7 +33,11 @@ CpuArch makeCpuArch(CpuVendor v, int family, int model) {
   if (v == CpuVendor::Intel) {
     if (family == 6 && model == 0x55) return CpuArch::IntelSkylakeX;
     if (family == 6 && (model == 0x6a || model == 0x6c)) return CpuArch::IntelIceLakeX;
-    if (family == 6 && (model == 0x8f || model == 0xcf)) return CpuArch::IntelSapphireRapids;
+    if (family == 6 && model == 0x8f) return CpuArch::IntelSapphireRapids;
+    if (family == 6 && model == 0xcf) return CpuArch::IntelEmeraldRapids;
+    if (family == 6 && (model == 0xad || model == 0xae)) return CpuArch::IntelGraniteRapids;
+    if (family == 6 && model == 0x3f) return CpuArch::IntelHaswellX;
+    if (family == 6 && (model == 0x4f || model == 0x56)) return CpuArch::IntelBroadwellX;
     return CpuArch::IntelGeneric;
   }
   if (v != CpuVendor::Amd) return CpuArch::Unknown;

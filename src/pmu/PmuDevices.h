@@ -33,7 +33,11 @@ enum class CpuArch {
   IntelGeneric,
   IntelSkylakeX,        // family 6 model 0x55: Skylake-SP / Cascade Lake / Cooper Lake
   IntelIceLakeX,        // 0x6a, 0x6c: Ice Lake-SP / -D
-  IntelSapphireRapids,  // 0x8f, 0xcf: Sapphire / Emerald Rapids
+  IntelSapphireRapids,  // 0x8f: Sapphire Rapids
+  IntelEmeraldRapids,   // 0xcf: Emerald Rapids (Raptor Cove: SPR's core events)
+  IntelGraniteRapids,   // 0xad, 0xae: Granite Rapids -AP/-SP, -D (Redwood Cove)
+  IntelHaswellX,        // 0x3f: Haswell-EP/EX
+  IntelBroadwellX,      // 0x4f, 0x56: Broadwell-EP/EX, Broadwell-DE
 };
 const char* cpuArchName(CpuArch a);
 CpuArch makeCpuArch(CpuVendor v, int family, int model);
