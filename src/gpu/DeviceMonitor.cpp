@@ -1,5 +1,6 @@
 #include "gpu/DeviceMonitor.h"
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <hsa/hsa.h>
 #include <time.h>
@@ -88,6 +89,7 @@ bool DeviceMonitor::start(const Json& cfg, std::string* err) {
       counterPasses_ = cfg.at("counter_passes").asString();
     if (cfg.contains("kfd_root") && cfg.at("kfd_root").isString()) kfdRoot_ = cfg.at("kfd_root").asString();
     if (cfg.contains("proc_root") && cfg.at("proc_root").isString()) procRoot_ = cfg.at("proc_root").asString();
+    resolver_ = PidResolver(procRoot_);
   }
   hz_ = std::max(1.0, hz_);
   // "auto" (default): the full lite set while every process on the GPU is
@@ -170,7 +172,14 @@ void DeviceMonitor::applyMasks(Gpu* g) {
 }
 
 void DeviceMonitor::checkVisibility(Gpu* g, size_t cp, uint64_t* prevTs, std::vector<double>* prev) {
-  GpuVisibility v = gpuVisibility(g->gpuId, static_cast<int>(getpid()), kfdRoot_, procRoot_);
+  GpuVisibility v;
+  {
+    std::lock_guard<std::mutex> lk(visMu_);
+    if (DIR* d = opendir((kfdRoot_ + "/proc").c_str())) {
+      closedir(d);
+      v = gpuVisibility(g->gpuId, static_cast<int>(getpid()), kfdProcesses(kfdRoot_), resolver_, procRoot_, monoNs());
+    }
+  }
   const bool limited = !v.full();
   bool switchTo = g->onAlt;
   {

@@ -88,6 +88,8 @@ class DeviceMonitor {
   double hz_ = 100.0;
   std::string counterSet_ = "auto", counterPasses_;
   bool auto_ = false;
+  std::mutex visMu_;
+  PidResolver resolver_;  // guarded by visMu_ (the GPUs' loop threads share it)
   std::string kfdRoot_ = "/sys/class/kfd/kfd", procRoot_ = "/proc";
   std::atomic<bool> stop_{false};
   std::vector<std::unique_ptr<Gpu>> gpus_;
