@@ -338,10 +338,16 @@ Json DeviceMonitor::config() {
     Json o = Json::object();
     o["device"] = g->index;
     Json ps = Json::array();
-    if (g->alt) {
+    {
       std::lock_guard<std::mutex> lk(g->mu);
-      o["sampling"] = g->onAlt ? "xproc" : "lite";
+      if (g->alt) o["sampling"] = g->onAlt ? "xproc" : "lite";
       o["counter_visibility"] = !g->vis.known ? "unknown" : g->limitedNow ? "limited" : "full";
+      Json pids = Json::array(), unc = Json::array();
+      for (int p : g->vis.pids) pids.push_back(p);
+      for (int p : g->vis.uncountable) unc.push_back(p);
+      o["compute_pids"] = pids;
+      o["uncountable_pids"] = unc;
+      o["gpu_bdf"] = pciLocString(g->pciLoc);
     }
     for (const auto& p : g->passes) {
       Json pj = Json::object();
