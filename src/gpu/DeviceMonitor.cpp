@@ -89,7 +89,6 @@ bool DeviceMonitor::start(const Json& cfg, std::string* err) {
       counterPasses_ = cfg.at("counter_passes").asString();
     if (cfg.contains("kfd_root") && cfg.at("kfd_root").isString()) kfdRoot_ = cfg.at("kfd_root").asString();
     if (cfg.contains("proc_root") && cfg.at("proc_root").isString()) procRoot_ = cfg.at("proc_root").asString();
-    resolver_ = PidResolver(procRoot_);
   }
   hz_ = std::max(1.0, hz_);
   // "auto" (default): the full lite set while every process on the GPU is
@@ -177,7 +176,18 @@ void DeviceMonitor::checkVisibility(Gpu* g, size_t cp, uint64_t* prevTs, std::ve
     std::lock_guard<std::mutex> lk(visMu_);
     if (DIR* d = opendir((kfdRoot_ + "/proc").c_str())) {
       closedir(d);
-      v = gpuVisibility(g->gpuId, static_cast<int>(getpid()), kfdProcesses(kfdRoot_), resolver_, procRoot_, monoNs());
+      // a full /proc scan is needed only under another PID numbering; at
+      // most once a second, shared by every GPU's thread
+      auto locals = [this]() -> const std::vector<LocalGpuProcess>& {
+        const uint64_t now = monoNs();
+        if (localScanNs_ == 0 || now - localScanNs_ > 1'000'000'000ull) {
+          localScan_ = localGpuProcesses(procRoot_);
+          localScanNs_ = now;
+        }
+        return localScan_;
+      };
+      v = gpuVisibility(g->gpuId, pciLocString(g->pciLoc), static_cast<int>(getpid()), kfdProcesses(kfdRoot_), locals,
+                        procRoot_);
     }
   }
   const bool limited = !v.full();
@@ -316,6 +326,7 @@ Json DeviceMonitor::drainRecords() {
       // whose work the counters could see (CounterVisibility.h)
       r["counter_visibility"] = !vis.known ? "unknown" : limited ? "limited" : "full";
       r["compute_pids"] = static_cast<unsigned long long>(vis.pids.size());
+      if (vis.foreign) r["foreign_processes"] = vis.foreign;  // other PID namespaces: not checkable
       if (!vis.uncountable.empty()) {
         std::string l;
         for (size_t i = 0; i < vis.uncountable.size() && i < 16; ++i) l += (i ? "," : "") + std::to_string(vis.uncountable[i]);

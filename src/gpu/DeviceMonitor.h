@@ -88,8 +88,9 @@ class DeviceMonitor {
   double hz_ = 100.0;
   std::string counterSet_ = "auto", counterPasses_;
   bool auto_ = false;
-  std::mutex visMu_;
-  PidResolver resolver_;  // guarded by visMu_ (the GPUs' loop threads share it)
+  std::mutex visMu_;  // the GPUs' loop threads share the /proc scan below
+  std::vector<LocalGpuProcess> localScan_;
+  uint64_t localScanNs_ = 0;
   std::string kfdRoot_ = "/sys/class/kfd/kfd", procRoot_ = "/proc";
   std::atomic<bool> stop_{false};
   std::vector<std::unique_ptr<Gpu>> gpus_;
