@@ -1,7 +1,9 @@
-# round 4 g04: overhead per counter set on the Llama-3-8B headline (1 kHz, pooled A/B and
-# vs no-agent children, + a countable-only child)
+# round 4 g04: overhead per counter set on the Llama-3-8B headline (1 kHz): the headline run
+# once per set in a fresh process (pooled A/B, vs its own no-agent children) + a countable-only
+# child.  (The first g04 run restarted the agent inside one process; its train step kept
+# calling the stopped first agent, so it was re-run this way.)  Two halves: g04a, g04b.
 set -o pipefail
-O=gpurun_out/g04; mkdir -p $O
+H=${1:-a}; O=gpurun_out/g04$H; mkdir -p $O
+if [ "$H" = a ]; then M="core,lite,full"; else M="lean,core:3/lite:1"; fi
 timeout -k 10 1100 python -u bench.py --steps 10 --warmup 3 --ab-rounds 6 --ab-steps 5 --host-pmu off \
-  --overhead-matrix "core,lean,lite,full,core:3/lite:1" --matrix-out $O/overhead_matrix.json \
-  > $O/matrix.out 2> $O/matrix.err
+  --overhead-matrix "$M" --matrix-out $O/overhead_matrix.json > $O/matrix.out 2> $O/matrix.err
