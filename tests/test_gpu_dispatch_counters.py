@@ -62,3 +62,51 @@ def test_dispatch_counters_gemm_and_copy(native_built):
     p = prec["dispatches"][0]["derived"]
     assert "fp32_active" in p and p["mfma_bf16_tflops"] > 100, prec
     assert st["samples_failed"] == 0
+
+
+def test_reduced_rate_hbm_pass_matches_dispatch_counting(native_built):
+    """HBM traffic read only in every fourth batch (pass plan core:3,lite:1:
+    the 256 TCC instances at a quarter of the sample rate) still prices a
+    steady 1 GiB copy loop: the sampled read / write GB/s of the copy phase
+    agree with exact per-dispatch counting of the same kernel and account for
+    the bytes the loop moved.  (Overhead matrix, profiles/round4/README.md.)"""
+    res = _run("""
+        from dynolog_amd import agent
+        agent.preinit(dispatch_counters=True)
+        import json, time, torch
+        torch.cuda.set_device(0)
+        src = torch.ones(1 << 28, dtype=torch.float32, device="cuda")   # 1 GiB
+        dst = torch.empty_like(src)
+        torch.add(src, 1.0, out=dst); torch.cuda.synchronize()
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, batch=8, sinks=("memory",),
+                                 counter_passes="core:3,lite:1")
+        n = 0
+        t0 = time.perf_counter()
+        with a.phase("copy"):
+            while time.perf_counter() - t0 < 3.0:
+                for _ in range(20):
+                    torch.add(src, 1.0, out=dst)
+                n += 20
+                torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+        time.sleep(0.3)
+        ps = a.phase_stats(); st = a.stats()
+        dc = agent.DispatchCounters(kernel_regex="elementwise", dispatches=2).start()
+        for _ in range(3):
+            torch.add(src, 1.0, out=dst)
+        torch.cuda.synchronize()
+        exact = dc.finish(timeout_s=20)
+        a.stop()
+        print("RESULT " + json.dumps(dict(ps=ps, st=st, exact=exact, n=n, wall=wall)))
+    """, timeout=300)
+    st, exact = res["st"], res["exact"]
+    copy = res["ps"]["0"]["copy"]
+    print(json.dumps(dict(copy=copy, exact=exact["dispatches"][0]["derived"], n=res["n"], wall=res["wall"]), indent=1))
+    assert st["samples_failed"] == 0 and [p["set"] for p in st["counter_passes"]] == ["core", "lite"], st
+    assert exact["counted"] == 2, exact
+    ex = exact["dispatches"][0]["derived"]
+    assert copy["hbm_read_gbps"] == pytest.approx(ex["hbm_read_gbps"], rel=0.15), (copy, ex)
+    assert copy["hbm_write_gbps"] == pytest.approx(ex["hbm_write_gbps"], rel=0.15), (copy, ex)
+    moved = (copy["hbm_read_gbps"] + copy["hbm_write_gbps"]) * 1e9 * res["wall"]
+    assert moved == pytest.approx(2.0 * (1 << 30) * res["n"], rel=0.2), (moved, res["n"])
