@@ -83,6 +83,15 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
     if (ev.count(kSpr))
       for (CpuArch a : {CpuArch::IntelEmeraldRapids, CpuArch::IntelGraniteRapids})
         if (!ev.count(a)) ev[a] = ev.at(kSpr);
+    // client cores share their server siblings' core encodings: Skylake (no
+    // AVX-512 forms) from Skylake-SP, Ice Lake client from Ice Lake-SP
+    if (ev.count(kSkx) && !ev.count(CpuArch::IntelSkylake)) {
+      std::vector<EventRef> v;
+      for (const auto& r : ev.at(kSkx))
+        if (r.spec.find("512b") == std::string::npos) v.push_back(r);
+      ev[CpuArch::IntelSkylake] = v;
+    }
+    if (ev.count(kIcx) && !ev.count(CpuArch::IntelIceLake)) ev[CpuArch::IntelIceLake] = ev.at(kIcx);
     if (ev.count(kSkx) && (id == "l2_cache_misses" || id == "tlb_misses" || id == "l3_cache_misses_per_instruction"))
       for (CpuArch a : {CpuArch::IntelHaswellX, CpuArch::IntelBroadwellX})
         if (!ev.count(a)) ev[a] = ev.at(kSkx);

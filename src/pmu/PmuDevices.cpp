@@ -25,6 +25,8 @@ const char* cpuArchName(CpuArch a) {
     case CpuArch::IntelGraniteRapids: return "intel_gnr";
     case CpuArch::IntelHaswellX: return "intel_hsx";
     case CpuArch::IntelBroadwellX: return "intel_bdx";
+    case CpuArch::IntelSkylake: return "intel_skl";
+    case CpuArch::IntelIceLake: return "intel_icl";
     default: return "unknown";
   }
 }
@@ -38,6 +40,10 @@ CpuArch makeCpuArch(CpuVendor v, int family, int model) {
     if (family == 6 && (model == 0xad || model == 0xae)) return CpuArch::IntelGraniteRapids;
     if (family == 6 && model == 0x3f) return CpuArch::IntelHaswellX;
     if (family == 6 && (model == 0x4f || model == 0x56)) return CpuArch::IntelBroadwellX;
+    if (family == 6 && (model == 0x4e || model == 0x5e || model == 0x8e || model == 0x9e || model == 0xa5 ||
+                        model == 0xa6))
+      return CpuArch::IntelSkylake;
+    if (family == 6 && (model == 0x7d || model == 0x7e)) return CpuArch::IntelIceLake;
     return CpuArch::IntelGeneric;
   }
   if (v != CpuVendor::Amd) return CpuArch::Unknown;

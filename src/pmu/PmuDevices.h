@@ -38,6 +38,9 @@ enum class CpuArch {
   IntelGraniteRapids,   // 0xad, 0xae: Granite Rapids -AP/-SP, -D (Redwood Cove)
   IntelHaswellX,        // 0x3f: Haswell-EP/EX
   IntelBroadwellX,      // 0x4f, 0x56: Broadwell-EP/EX, Broadwell-DE
+  IntelSkylake,         // 0x4e, 0x5e, 0x8e, 0x9e, 0xa5, 0xa6: Skylake / Kaby / Coffee / Comet Lake
+                        // client (Skylake-SP's core encodings, no AVX-512)
+  IntelIceLake,         // 0x7d, 0x7e: Ice Lake client (Ice Lake-SP's core encodings)
 };
 const char* cpuArchName(CpuArch a);
 CpuArch makeCpuArch(CpuVendor v, int family, int model);
