@@ -681,8 +681,8 @@ def test_host_and_device_pack_modes_agree(native_built):
             recs = [r for r in a.memory_records() if "mfma_util" in r and r.get("counter_samples", 0) > 100]
             st = a.stats()
             a.stop()
-            out[pack] = dict(st=st, names=names, mfma=[r["mfma_util"] for r in recs],
-                             tflops=[r["mfma_bf16_tflops"] for r in recs])
+            out[pack] = dict(st=st, names=names, mfma=[float(r["mfma_util"]) for r in recs],
+                             tflops=[float(r["mfma_bf16_tflops"]) for r in recs])
         print("RESULT " + json.dumps(out))
     """)
     h, d = res["host"], res["device"]
