@@ -1884,6 +1884,7 @@ Json Agent::stats() const {
     }
     j["counter_passes"] = ps;
     j["pack_mode"] = cfg_.packMode;
+    j["dispatch_counting_started"] = DispatchCounters::get().everStarted();
     const uint64_t sw = passSwitches_.load();
     j["pass_switches"] = static_cast<unsigned long long>(sw);
     j["pass_switch_us_avg"] = sw ? passSwitchNs_.load() / static_cast<double>(sw) * 1e-3 : 0.0;
