@@ -45,7 +45,7 @@ SLOT_DTYPE = np.dtype([
     ("seq", "<u8"), ("host_ts_ns", "<u8"), ("gpu_pack_ticks", "<u8"),
     ("rank", "<u4"), ("flags", "<u4"),
     ("delta", "<u8", (MAX_COUNTERS,)), ("derived", "<f4", (MAX_DERIVED,)),
-    ("sample_latency_ns", "<u4"), ("n_records", "<u4"), ("phase", "<u4"), ("pass", "<u4"), ("reserved", "<u4", (4,)),
+    ("sample_latency_ns", "<u4"), ("n_records", "<u4"), ("phase", "<u4"), ("pass", "<u4"), ("counter_mask", "<u4"), ("reserved", "<u4", (3,)),
 ])
 assert SLOT_DTYPE.itemsize == SLOT_BYTES
 

@@ -171,6 +171,7 @@ class Agent {
     int* dSegStart = nullptr;
     int* dSegLen = nullptr;
     std::vector<int> counterOf;  // record index -> counter slot (host pack)
+    uint32_t counterMask = 0;    // delta[] positions this set selects (every slot carries it)
   };
   bool setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::string* err);
   void switchPass();  // sampler thread: stop the current pass, start the next
