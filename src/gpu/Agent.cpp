@@ -872,11 +872,17 @@ bool Agent::step(hipStream_t stream, std::string* err) {
   // hanging or crashing the trainer. Same program point on every rank.
   ncclResult_t async = ncclSuccess;
   if (comm_) ncclCommGetAsyncError(comm_, &async);
+  // A non-blocking communicator still busy with the previous call (RCCL
+  // connects the gather's peers in the background after the first
+  // ncclGather returned): no new call may be issued until it has settled.
+  if (comm_ && async == ncclInProgress)
+    async = static_cast<ncclResult_t>(ncclSettle(ncclInProgress, 60'000'000'000ull));
   const bool injected = cfg_.faultGatherAtStep > 0 && steps_ >= cfg_.faultGatherAtStep;
-  if ((async != ncclSuccess && async != ncclInProgress) || injected) {
+  if (async != ncclSuccess || injected) {
     gatherFailed_ = true;
     lastError_ = injected ? "injected gather fault at step " + std::to_string(steps_.load())
-                          : std::string("RCCL async error: ") + ncclGetErrorString(async);
+                 : async == ncclInProgress ? std::string("RCCL communicator still busy after 60 s")
+                                           : std::string("RCCL async error: ") + ncclGetErrorString(async);
     LOG(ERROR) << "GPU agent rank " << cfg_.rank << ": " << lastError_
                << "; counter gathers disabled, sampling continues locally";
     if (comm_ && !injected) {
@@ -1095,6 +1101,16 @@ bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err
   if (r != ncclSuccess) {
     if (err) *err = std::string("ncclAllReduce (gather size): ") + ncclGetErrorString(r);
     return false;
+  }
+  // the call returned; the communicator may still be connecting in the background
+  {
+    ncclResult_t st = ncclSuccess;
+    ncclCommGetAsyncError(comm_, &st);
+    if (st == ncclInProgress) st = static_cast<ncclResult_t>(ncclSettle(ncclInProgress, kCollTimeoutNs));
+    if (st != ncclSuccess) {
+      if (err) *err = std::string("agent communicator after ncclAllReduce: ") + ncclGetErrorString(st);
+      return false;
+    }
   }
   if (cfg_.gatherMode == "allgather") r = ncclAllGather(dSend_, recv, block, ncclUint8, comm_, stream);
   else if (cfg_.forceNonRoot) r = ncclGather(dSend_, dSend_, block, ncclUint8, 0, comm_, stream);  // 1-rank test: in place
@@ -1734,8 +1750,13 @@ void Agent::stop() {
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
   hipWarn(hipDeviceSynchronize(), "device sync at stop");
   if (comm_) {
-    // non-blocking communicator: finalize (flush), bounded, then free
-    if (ncclSettle(ncclCommFinalize(comm_), 10'000'000'000ull) == ncclSuccess) ncclCommDestroy(comm_);
+    // non-blocking communicator: let a call still in progress settle, then
+    // finalize (flush), bounded, then free
+    ncclResult_t st = ncclSuccess;
+    ncclCommGetAsyncError(comm_, &st);
+    if (st == ncclInProgress) st = static_cast<ncclResult_t>(ncclSettle(ncclInProgress, 10'000'000'000ull));
+    if (st == ncclSuccess && ncclSettle(ncclCommFinalize(comm_), 10'000'000'000ull) == ncclSuccess)
+      ncclCommDestroy(comm_);
     else ncclCommAbort(comm_);
     comm_ = nullptr;
   }
