@@ -205,6 +205,10 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     *err = "agent already running";
     return false;
   }
+  if (stuckThreads_) {
+    *err = "an earlier stop() left a GPU agent thread stuck in the runtime; restart the process";
+    return false;
+  }
   if (cfg.world < 1 || cfg.rank < 0 || cfg.rank >= cfg.world ||
       (!cfg.rankLabels.empty() && static_cast<int>(cfg.rankLabels.size()) != cfg.world)) {
     *err = "bad gather group: rank " + std::to_string(cfg.rank) + " of " + std::to_string(cfg.world) + " with " +
@@ -568,8 +572,16 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   // set here, not in the sampler thread: a set_rate() right after start
   // must not be overwritten when the thread comes up
   setSampleHz(cfg_.sampleHz);
-  samplerThread_ = std::thread([this] { samplerLoop(); });
-  if (root) consumerThread_ = std::thread([this] { consumerLoop(); });
+  samplerDone_ = consumerDone_ = ctlDone_ = false;
+  samplerThread_ = std::thread([this] {
+    samplerLoop();
+    samplerDone_ = true;
+  });
+  if (root)
+    consumerThread_ = std::thread([this] {
+      consumerLoop();
+      consumerDone_ = true;
+    });
   // Keep the sampler (and drain consumer) on CPUs NUMA-local to this GPU: its
   // H2D staging copies and the CP round trip of every sample stay on the
   // socket that owns the PCIe root of the device.
@@ -594,7 +606,11 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   pinnedCpus_ = pinned;
   if (cfg_.daemonControl) {
     ctl_ = ipc::Fabric::create("dynoagent_" + std::to_string(getpid()) + "_r" + std::to_string(cfg_.rank));
-    if (ctl_) ctlThread_ = std::thread([this] { controlLoop(); });
+    if (ctl_)
+      ctlThread_ = std::thread([this] {
+        controlLoop();
+        ctlDone_ = true;
+      });
     else LOG(WARNING) << "GPU agent: daemon control endpoint unavailable";
   }
   LOG(INFO) << "GPU agent started: rank " << cfg_.rank << "/" << cfg_.world << " device "
@@ -1740,9 +1756,31 @@ void Agent::stop() {
   stopFlag_ = true;
   cv_.notify_all();
   samplerClockValid_ = consumerClockValid_ = false;  // the clock ids die with the threads
-  if (samplerThread_.joinable()) samplerThread_.join();
-  if (consumerThread_.joinable()) consumerThread_.join();
-  if (ctlThread_.joinable()) ctlThread_.join();
+  // Bounded joins: a thread stuck inside the runtime (a counter read whose
+  // completion never arrives) must not hang the trainer's exit.  A thread
+  // still running after the deadline is detached and the state it may still
+  // touch is kept (leaked) instead of freed.
+  bool stuck = false;
+  auto boundedJoin = [&](std::thread& t, std::atomic<bool>& done, const char* what) {
+    if (!t.joinable()) return;
+    const uint64_t deadline = monoNs() + 10'000'000'000ull;
+    while (!done.load() && monoNs() < deadline) usleep(1000);
+    if (done.load()) {
+      t.join();
+    } else {
+      LOG(ERROR) << "GPU agent stop: the " << what << " thread did not finish within 10 s; detached (its buffers are kept)";
+      t.detach();
+      stuck = true;
+    }
+  };
+  boundedJoin(samplerThread_, samplerDone_, "sampler");
+  boundedJoin(consumerThread_, consumerDone_, "consumer");
+  boundedJoin(ctlThread_, ctlDone_, "control");
+  if (stuck) {
+    stuckThreads_ = true;
+    running_ = false;
+    return;
+  }
   ctl_.reset();
   slotProd_.reset();
   slotRing_.reset();  // unlinks the shm segments (the Agent itself is never destroyed)

@@ -206,6 +206,8 @@ class Agent {
   // a sampler this many periods behind drops the missed ticks; less is caught up
   static constexpr uint64_t kMaxCatchUpTicks = 4;
   std::thread samplerThread_, consumerThread_, ctlThread_;
+  std::atomic<bool> samplerDone_{false}, consumerDone_{false}, ctlDone_{false};  // set as each thread exits
+  bool stuckThreads_ = false;  // a stop() had to detach a thread: no restart in this process
   std::unique_ptr<ipc::Fabric> ctl_;
 
   // device buffers

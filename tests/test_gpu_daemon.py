@@ -257,6 +257,7 @@ def test_gpusqtt_rpc_through_agent(native_built, tmp_path):
                 y = x @ x
             torch.cuda.synchronize()
             a.step()
+        print("LOOP_DONE", flush=True)
         st = a.stats()
         a.stop()
         print("STATS", st["samples_taken"], st["samples_failed"], flush=True)
@@ -293,7 +294,12 @@ def test_gpusqtt_rpc_through_agent(native_built, tmp_path):
                 assert sum(f.endswith(".att") for f in files) >= 2, files
             finally:
                 open(done, "w").close()
-                so, _ = p.communicate(timeout=60)
+                try:
+                    so, _ = p.communicate(timeout=60)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    so, se = p.communicate(timeout=30)
+                    raise AssertionError("agent child hung at exit:\n" + so[-1500:] + "\n" + se[-6000:])
             stats = [l for l in so.splitlines() if l.startswith("STATS")]
             assert stats and int(stats[0].split()[2]) == 0, so[-2000:]  # sampling resumed cleanly
     finally:
@@ -306,6 +312,8 @@ def test_gpupmc_rpc_through_agent(native_built, tmp_path):
     sockdir = tempfile.mkdtemp(prefix="dy", dir="/tmp")
     env = {"KINETO_IPC_SOCKET_DIR": sockdir}
     code = textwrap.dedent("""
+        import faulthandler
+        faulthandler.dump_traceback_later(50, exit=False)  # names the blocking call if the child hangs
         from dynolog_amd import agent
         agent.preinit(dispatch_counters=True)
         import os, time, torch
@@ -318,6 +326,7 @@ def test_gpupmc_rpc_through_agent(native_built, tmp_path):
                 y = x @ x
             torch.cuda.synchronize()
             a.step()
+        print("LOOP_DONE", flush=True)
         st = a.stats()
         a.stop()
         print("STATS", st["samples_taken"], st["samples_failed"], flush=True)
@@ -352,7 +361,12 @@ def test_gpupmc_rpc_through_agent(native_built, tmp_path):
                 assert res["dispatches"][0]["counters"]["SQ_INSTS_VALU_MFMA_MOPS_BF16"] > 0, res
             finally:
                 open(done, "w").close()
-                so, _ = p.communicate(timeout=60)
+                try:
+                    so, _ = p.communicate(timeout=60)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    so, se = p.communicate(timeout=30)
+                    raise AssertionError("agent child hung at exit:\n" + so[-1500:] + "\n" + se[-6000:])
             stats = [l for l in so.splitlines() if l.startswith("STATS")]
             assert stats and int(stats[0].split()[2]) == 0, so[-2000:]
     finally:
