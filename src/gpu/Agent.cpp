@@ -806,7 +806,9 @@ void Agent::samplerLoop() {
     // attributed to it
     const uint32_t phase = hPhase_ ? __atomic_load_n(hPhase_, __ATOMIC_ACQUIRE) : 0;
     const uint64_t t0 = monoNs();
+    sampleStartNs_.store(t0, std::memory_order_relaxed);
     bool ok = sampler_->sample(raw, &n, nullptr, &err);
+    sampleStartNs_.store(0, std::memory_order_relaxed);
     const uint64_t t1 = monoNs();
     if (!ok || n != R) {
       samplesFailed_++;
@@ -1768,7 +1770,10 @@ void Agent::stop() {
     if (done.load()) {
       t.join();
     } else {
-      LOG(ERROR) << "GPU agent stop: the " << what << " thread did not finish within 10 s; detached (its buffers are kept)";
+      const uint64_t inFlight = sampleStartNs_.load();
+      LOG(ERROR) << "GPU agent stop: the " << what << " thread did not finish within 10 s; detached (its buffers are kept)"
+                 << (inFlight ? "; a counter read has been waiting " + std::to_string((monoNs() - inFlight) / 1000000) + " ms"
+                              : std::string());
       t.detach();
       stuck = true;
     }
@@ -1968,6 +1973,9 @@ Json Agent::stats() const {
     }
     j["counter_passes"] = ps;
     j["pack_mode"] = cfg_.packMode;
+    // a counter read still waiting for the command processor (a stuck read shows here)
+    const uint64_t inFlight = sampleStartNs_.load(std::memory_order_relaxed);
+    j["sample_in_flight_ms"] = inFlight ? (monoNs() - inFlight) * 1e-6 : 0.0;
     j["dispatch_counting_started"] = DispatchCounters::get().everStarted();
     const uint64_t sw = passSwitches_.load();
     j["pass_switches"] = static_cast<unsigned long long>(sw);

@@ -207,7 +207,8 @@ class Agent {
   static constexpr uint64_t kMaxCatchUpTicks = 4;
   std::thread samplerThread_, consumerThread_, ctlThread_;
   std::atomic<bool> samplerDone_{false}, consumerDone_{false}, ctlDone_{false};  // set as each thread exits
-  bool stuckThreads_ = false;  // a stop() had to detach a thread: no restart in this process
+  bool stuckThreads_ = false;
+  std::atomic<uint64_t> sampleStartNs_{0};  // start of the counter read in flight (0: none)  // a stop() had to detach a thread: no restart in this process
   std::unique_ptr<ipc::Fabric> ctl_;
 
   // device buffers

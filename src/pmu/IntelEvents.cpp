@@ -96,7 +96,7 @@ bool isIntelArch(CpuArch a) {
   return a == CpuArch::IntelGeneric || a == CpuArch::IntelSkylakeX || a == CpuArch::IntelIceLakeX ||
          a == CpuArch::IntelSapphireRapids || a == CpuArch::IntelEmeraldRapids || a == CpuArch::IntelGraniteRapids ||
          a == CpuArch::IntelHaswellX || a == CpuArch::IntelBroadwellX || a == CpuArch::IntelSkylake ||
-         a == CpuArch::IntelIceLake;
+         a == CpuArch::IntelIceLake || a == CpuArch::IntelHaswell || a == CpuArch::IntelBroadwell;
 }
 
 bool isSprLike(CpuArch a) {
@@ -110,9 +110,11 @@ std::vector<AmdEventDef> intelEventTable(CpuArch arch) {
   if (!isIntelArch(arch)) return v;
   v.insert(v.end(), std::begin(kArch), std::end(kArch));
   if (arch == CpuArch::IntelGeneric) return v;
-  if (arch == CpuArch::IntelHaswellX || arch == CpuArch::IntelBroadwellX) {
+  if (arch == CpuArch::IntelHaswellX || arch == CpuArch::IntelBroadwellX || arch == CpuArch::IntelHaswell ||
+      arch == CpuArch::IntelBroadwell) {
     v.insert(v.end(), std::begin(kHswBdw), std::end(kHswBdw));
-    if (arch == CpuArch::IntelBroadwellX) v.insert(v.end(), std::begin(kBdwFp), std::end(kBdwFp));
+    if (arch == CpuArch::IntelBroadwellX || arch == CpuArch::IntelBroadwell)
+      v.insert(v.end(), std::begin(kBdwFp), std::end(kBdwFp));
     return v;
   }
   for (const auto& e : kFp)  // client Skylake has no 512-bit forms

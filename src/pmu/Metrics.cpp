@@ -93,7 +93,7 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
     }
     if (ev.count(kIcx) && !ev.count(CpuArch::IntelIceLake)) ev[CpuArch::IntelIceLake] = ev.at(kIcx);
     if (ev.count(kSkx) && (id == "l2_cache_misses" || id == "tlb_misses" || id == "l3_cache_misses_per_instruction"))
-      for (CpuArch a : {CpuArch::IntelHaswellX, CpuArch::IntelBroadwellX})
+      for (CpuArch a : {CpuArch::IntelHaswellX, CpuArch::IntelBroadwellX, CpuArch::IntelHaswell, CpuArch::IntelBroadwell})
         if (!ev.count(a)) ev[a] = ev.at(kSkx);
     auto m = std::make_shared<MetricDesc>();
     m->id = std::move(id);
@@ -316,10 +316,12 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
     return v;
   };
   add("fp_instrs_single_precision", "Single-precision FP FLOPs retired (scalar + packed, by vector width)",
-      {{kSkx, fpSingle}, {kIcx, fpSingle}, {kSpr, fpSingle}, {CpuArch::IntelBroadwellX, no512(fpSingle)}},
+      {{kSkx, fpSingle}, {kIcx, fpSingle}, {kSpr, fpSingle}, {CpuArch::IntelBroadwellX, no512(fpSingle)},
+       {CpuArch::IntelBroadwell, no512(fpSingle)}},
       [](const auto& c, double s, double, auto& o) { o["fp_single_gflops"] = ratio(get(c, "flops"), s) * 1e-9; });
   add("fp_instrs_double_precision", "Double-precision FP FLOPs retired (scalar + packed, by vector width)",
-      {{kSkx, fpDouble}, {kIcx, fpDouble}, {kSpr, fpDouble}, {CpuArch::IntelBroadwellX, no512(fpDouble)}},
+      {{kSkx, fpDouble}, {kIcx, fpDouble}, {kSpr, fpDouble}, {CpuArch::IntelBroadwellX, no512(fpDouble)},
+       {CpuArch::IntelBroadwell, no512(fpDouble)}},
       [](const auto& c, double s, double, auto& o) { o["fp_double_gflops"] = ratio(get(c, "flops"), s) * 1e-9; });
   std::vector<EventRef> br = {{"brn", "cpu:ex_ret_brn"},
                               {"brn_misp", "cpu:ex_ret_brn_misp"},

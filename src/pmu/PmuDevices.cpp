@@ -27,6 +27,8 @@ const char* cpuArchName(CpuArch a) {
     case CpuArch::IntelBroadwellX: return "intel_bdx";
     case CpuArch::IntelSkylake: return "intel_skl";
     case CpuArch::IntelIceLake: return "intel_icl";
+    case CpuArch::IntelHaswell: return "intel_hsw";
+    case CpuArch::IntelBroadwell: return "intel_bdw";
     default: return "unknown";
   }
 }
@@ -44,6 +46,8 @@ CpuArch makeCpuArch(CpuVendor v, int family, int model) {
                         model == 0xa6))
       return CpuArch::IntelSkylake;
     if (family == 6 && (model == 0x7d || model == 0x7e)) return CpuArch::IntelIceLake;
+    if (family == 6 && (model == 0x3c || model == 0x45 || model == 0x46)) return CpuArch::IntelHaswell;
+    if (family == 6 && (model == 0x3d || model == 0x47)) return CpuArch::IntelBroadwell;
     return CpuArch::IntelGeneric;
   }
   if (v != CpuVendor::Amd) return CpuArch::Unknown;

@@ -41,6 +41,8 @@ enum class CpuArch {
   IntelSkylake,         // 0x4e, 0x5e, 0x8e, 0x9e, 0xa5, 0xa6: Skylake / Kaby / Coffee / Comet Lake
                         // client (Skylake-SP's core encodings, no AVX-512)
   IntelIceLake,         // 0x7d, 0x7e: Ice Lake client (Ice Lake-SP's core encodings)
+  IntelHaswell,         // 0x3c, 0x45, 0x46: Haswell client (Haswell-EP's core encodings)
+  IntelBroadwell,       // 0x3d, 0x47: Broadwell client (Broadwell-EP's core encodings)
 };
 const char* cpuArchName(CpuArch a);
 CpuArch makeCpuArch(CpuVendor v, int family, int model);
