@@ -421,7 +421,8 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     HIP_OK(hipMemsetAsync(dZero_, 0, R_ * sizeof(double), packStream_), "memset zero");
   }
   const size_t stageBytes = B * sizeof(DynoStageMeta) + B * R_ * sizeof(double);
-  nStage_ = std::clamp(cfg_.stages, 2, kMaxStage);
+  // host packing reduces a batch before its buffer is reused: two are plenty
+  nStage_ = hostPack_ ? 2 : std::clamp(cfg_.stages, 2, kMaxStage);
   for (int i = 0; i < nStage_; ++i) {
     if (!hStage_[i]) {  // kept across stop()/start() of the process-wide agent
       HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hStage_[i]), stageBytes, hipHostMallocDefault),
