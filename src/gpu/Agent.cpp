@@ -579,6 +579,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   // must not be overwritten when the thread comes up
   setSampleHz(cfg_.sampleHz);
   samplerDone_ = consumerDone_ = ctlDone_ = false;
+  samplerParked_ = false;
   samplerThread_ = std::thread([this] {
     samplerLoop();
     samplerDone_ = true;
@@ -769,11 +770,13 @@ void Agent::samplerLoop() {
         sampler_->stop();
         wasPaused = true;
       }
+      samplerParked_.store(true, std::memory_order_release);  // holdSampler() waits for this
       usleep(2000);
       next = monoNs();
       continue;
     }
     if (wasPaused) {
+      samplerParked_.store(false, std::memory_order_release);
       sampler_->select();
       if (!sampler_->start(&err)) {
         lastError_ = err;
@@ -1379,7 +1382,15 @@ int Agent::ncclSettle(int result, uint64_t timeoutNs) {
 void Agent::pause() { paused_ = true; }
 bool Agent::holdSampler() {
   if (samplerHold_.exchange(true)) return false;
-  usleep(5000);  // the sampler loop stops its counting context within ~2 ms
+  // A capture programs the same counters: it may start only once the sampler
+  // loop has stopped its device-counting context (a read still in flight
+  // when another counting context starts can wait forever).  Normally ~1 ms.
+  const uint64_t deadline = monoNs() + 2'000'000'000ull;
+  while (running_ && samplerThread_.joinable() && !samplerParked_.load(std::memory_order_acquire) &&
+         monoNs() < deadline)
+    usleep(200);
+  if (running_ && !samplerParked_.load())
+    LOG(WARNING) << "GPU agent: the sampler did not park within 2 s for an on-demand capture";
   return true;
 }
 void Agent::resume() { paused_ = false; }
