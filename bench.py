@@ -540,6 +540,8 @@ def main(argv=None) -> int:
         for _ in range(args.warmup):
             train_step()
         torch.cuda.synchronize()
+        # host memory after warm-up, against the end of the run (agent stats)
+        rss_start = ag.stats().get("host_rss_mb") if ag is not None else None
 
         base_s = None
         pooled_active_s = None
@@ -745,8 +747,10 @@ def main(argv=None) -> int:
                              "gather_latency_us_max", "gather_latency_samples", "gather_bytes",
                              "gather_slots", "gather_cap_slots_now", "gather_backlog", "drain_bytes",
                              "counter_passes", "pass_switches", "pass_switch_us_avg",
-                             "sampler_cpu_pct", "consumer_cpu_pct")
+                             "sampler_cpu_pct", "consumer_cpu_pct", "pack_mode", "host_rss_mb",
+                             "heap_in_use_mb")
                             if k in agent_stats}
+            out["agent"]["host_rss_mb_after_warmup"] = rss_start
         if args.host_pmu != "off":
             # one co-sampler per node (local rank 0): every node's summary
             # reaches the result line, keyed by host when there are several
