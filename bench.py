@@ -113,8 +113,11 @@ def parse_args(argv=None):
     p.add_argument("--sweep-out", default="", help="JSON file for the --sweep-hz table")
     p.add_argument("--no-agent-baseline", default="auto", choices=["auto", "on", "off"],
                    help="time the workload in child processes that never load the agent (no "
-                        "rocprofiler tool, no buffers): one before this run and one after it, the "
+                        "rocprofiler tool, no buffers): before this run and after it (--no-agent-children each), the "
                         "baseline BASELINE.md defines -> overhead_vs_no_agent_pct (auto = on with the agent)")
+    p.add_argument("--no-agent-children", type=int, default=2,
+                   help="no-agent children per side (before / after): the cross-process comparison "
+                        "carries a few tenths of a percent of process-to-process spread, averaged down")
     p.add_argument("--overhead-matrix", default="",
                    help="instead of the headline: price sampling per counter set, e.g. "
                         "'core,lean,lite,full,core:3/lite:1' (an entry with ':' is a pass plan, '/' between "
@@ -127,17 +130,22 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
-def baseline_child_env(environ) -> dict:
+def baseline_child_env(environ, seq: int = 0) -> dict:
     """Environment of a no-agent child.  Under torchrun the children form
-    their own group on MASTER_PORT + 100, and rank 0's child must host that
-    store itself: torchrun's TORCHELASTIC_USE_AGENT_STORE=True would make
-    every child a client of an agent store that does not exist on that port
-    (all of them would wait for the rendezvous timeout)."""
+    their own group on MASTER_PORT + 100 (+ the child's sequence number, so
+    back-to-back children never wait for the previous store's port), and
+    rank 0's child must host that store itself: torchrun's
+    TORCHELASTIC_USE_AGENT_STORE=True would make every child a client of an
+    agent store that does not exist on that port (all of them would wait for
+    the rendezvous timeout)."""
     env = dict(environ)
     if int(env.get("WORLD_SIZE", "1")) > 1:
-        env["MASTER_PORT"] = str(int(env.get("MASTER_PORT", "29511")) + 100)
+        env["MASTER_PORT"] = str(int(env.get("MASTER_PORT", "29511")) + 100 + seq)
         env["TORCHELASTIC_USE_AGENT_STORE"] = "False"
     return env
+
+
+_child_seq = [0]  # no-agent children started by this rank (same order on every rank)
 
 
 def run_baseline_child(args, tag: str, countable: bool = False) -> dict:
@@ -155,7 +163,8 @@ def run_baseline_child(args, tag: str, countable: bool = False) -> dict:
            "--micro-batch", str(args.micro_batch), "--seq-len", str(args.seq_len),
            "--optimizer", args.optimizer, "--batches", str(args.batches), "--host-pmu", "off",
            "--no-agent-baseline", "off", "--json-out", path]
-    env = baseline_child_env(os.environ)
+    env = baseline_child_env(os.environ, _child_seq[0])
+    _child_seq[0] += 1
     env.pop("ROCP_TOOL_LIBRARIES", None)
     if countable:
         # the job-side opt-in alone: a counting context configured, never started
@@ -414,7 +423,8 @@ def main(argv=None) -> int:
     no_agent_runs = []
     if want_no_agent:
         # before this process touches the GPU: nothing of ours is resident yet
-        no_agent_runs.append(run_baseline_child(args, "before"))
+        for i in range(max(1, args.no_agent_children)):
+            no_agent_runs.append(run_baseline_child(args, "before" if i == 0 else f"before{i + 1}"))
     if use_agent:
         from dynolog_amd import agent as dagent
         # rocprofiler-sdk tool registration: before HIP init.  Only this rank's
@@ -658,7 +668,8 @@ def main(argv=None) -> int:
             gc.collect()
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
-            no_agent_runs.append(run_baseline_child(args, "after"))
+            for i in range(max(1, args.no_agent_children)):
+                no_agent_runs.append(run_baseline_child(args, "after" if i == 0 else f"after{i + 1}"))
             pdist.barrier()
         window_s = (m1 - m0) * 1e-9 if ag is not None else meas_s
         value = total_samples / window_s if window_s > 0 else 0.0

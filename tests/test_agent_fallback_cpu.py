@@ -170,6 +170,7 @@ def test_baseline_child_env_hosts_its_own_store():
                                 "TORCHELASTIC_USE_AGENT_STORE": "True"})
     assert env["MASTER_PORT"] == "29600" and env["TORCHELASTIC_USE_AGENT_STORE"] == "False"
     assert env["RANK"] == "3"
+    assert b.baseline_child_env({"WORLD_SIZE": "8", "MASTER_PORT": "29500"}, 3)["MASTER_PORT"] == "29603"
     one = b.baseline_child_env({"WORLD_SIZE": "1", "MASTER_PORT": "29500"})
     assert one["MASTER_PORT"] == "29500" and "TORCHELASTIC_USE_AGENT_STORE" not in one
 
