@@ -58,7 +58,7 @@ def test_two_rank_ddp_bench_rehearsal(native_built):
     assert out["agent"]["samples_taken"] > 0 and out["agent"]["samples_failed"] == 0
     # the no-agent children (before / after) ran as their own 2-rank group
     runs = out["no_agent_runs"]
-    assert [x["tag"] for x in runs] == ["before", "after"], runs
+    assert [x["tag"] for x in runs] == ["before", "before2", "after", "after2"], runs
     assert all(x.get("rc") == 0 and x.get("ms_per_step", 0) > 0 for x in runs), runs
     assert out["overhead_vs_no_agent_pct"] is not None
 
@@ -152,7 +152,7 @@ def test_rccl_collective_gather_across_fake_hosts(native_built, mode, world, nod
                                               for x in out["ranks"]), out["ranks"]
     if children:
         runs = out["no_agent_runs"]
-        assert [x["tag"] for x in runs] == ["before", "after"], runs
+        assert [x["tag"] for x in runs] == ["before", "before2", "after", "after2"], runs
         assert all(x.get("rc") == 0 and x.get("ms_per_step", 0) > 0 for x in runs), runs
         assert out["overhead_vs_no_agent_pct"] is not None
     assert "gather_fallback" not in out and out["config"]["gather"] == mode, out
