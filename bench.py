@@ -118,6 +118,11 @@ def parse_args(argv=None):
     p.add_argument("--no-agent-children", type=int, default=2,
                    help="no-agent children per side (before / after): the cross-process comparison "
                         "carries a few tenths of a percent of process-to-process spread, averaged down")
+    p.add_argument("--child-started-once", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--child-probe", type=int, default=0,
+                   help="instead of the headline: N rounds of no-agent children (plain; agent started and "
+                        "stopped before the workload; libdyno_countable.so only), to price a counting "
+                        "context that has been started once against one never started")
     p.add_argument("--overhead-matrix", default="",
                    help="instead of the headline: price sampling per counter set, e.g. "
                         "'core,lean,lite,full,core:3/lite:1' (an entry with ':' is a pass plan, '/' between "
@@ -148,7 +153,7 @@ def baseline_child_env(environ, seq: int = 0) -> dict:
 _child_seq = [0]  # no-agent children started by this rank (same order on every rank)
 
 
-def run_baseline_child(args, tag: str, countable: bool = False) -> dict:
+def run_baseline_child(args, tag: str, countable: bool = False, started_once: bool = False) -> dict:
     """Times the same workload (model, batch, sequence, optimizer, steps) in a
     child process that never loads the agent: no rocprofiler-sdk tool is
     registered, no agent buffers exist.  Under torchrun every rank starts its
@@ -163,6 +168,8 @@ def run_baseline_child(args, tag: str, countable: bool = False) -> dict:
            "--micro-batch", str(args.micro_batch), "--seq-len", str(args.seq_len),
            "--optimizer", args.optimizer, "--batches", str(args.batches), "--host-pmu", "off",
            "--no-agent-baseline", "off", "--json-out", path]
+    if started_once:
+        cmd += ["--child-started-once", "--pack-mode", args.pack_mode, "--sample-hz", str(args.sample_hz)]
     env = baseline_child_env(os.environ, _child_seq[0])
     _child_seq[0] += 1
     env.pop("ROCP_TOOL_LIBRARIES", None)
@@ -175,6 +182,8 @@ def run_baseline_child(args, tag: str, countable: bool = False) -> dict:
         # the child's stdout goes to stderr: rank 0's stdout carries ONE result line
         r = subprocess.run(cmd, env=env, stdout=sys.stderr, timeout=600)
         res = {"tag": tag, "rc": r.returncode, "wall_s": round(time.time() - t0, 1), "countable": countable}
+        if started_once:
+            res["started_once"] = True
         if r.returncode == 0 and os.path.getsize(path) > 0:
             with open(path) as f:
                 res["ms_per_step"] = json.loads(f.read())["ms_per_step"]
@@ -330,6 +339,32 @@ def summarize_kernel_windows(kwin: dict, steps: int) -> dict:
     return out
 
 
+def run_child_probe(args) -> int:
+    """--child-probe N: N rounds of (plain, started-once, countable) no-agent
+    children, interleaved so box drift hits every kind alike."""
+    runs = []
+    for i in range(args.child_probe):
+        runs.append(run_baseline_child(args, f"plain{i}"))
+        runs.append(run_baseline_child(args, f"started_once{i}", started_once=True))
+        runs.append(run_baseline_child(args, f"countable{i}", countable=True))
+        print("probe", json.dumps(runs[-3:]), file=sys.stderr, flush=True)
+    def mean(kind):
+        v = [r["ms_per_step"] for r in runs if "ms_per_step" in r and r["tag"].startswith(kind)]
+        return sum(v) / len(v) if v else None
+    plain = mean("plain")
+    out = {"mode": "child_probe", "rounds": args.child_probe, "runs": runs, "plain_ms_per_step": plain}
+    for kind in ("started_once", "countable"):
+        m = mean(kind)
+        out[kind + "_ms_per_step"] = m
+        out[kind + "_vs_plain_pct"] = round((m / plain - 1.0) * 100.0, 3) if m and plain else None
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(line + "\n")
+    return 0
+
+
 def run_overhead_matrix(args) -> int:
     """--overhead-matrix: the headline run once per counter set (or pass
     plan), each in a fresh process exactly as the driver runs it (its own
@@ -416,6 +451,8 @@ def main(argv=None) -> int:
 
     if args.overhead_matrix:
         return run_overhead_matrix(args)  # spawns the runs; no GPU use here
+    if args.child_probe:
+        return run_child_probe(args)  # spawns the runs; no GPU use here
     use_agent = not args.no_agent
     if args.baseline_child:
         args.host_pmu = "off"
@@ -438,6 +475,9 @@ def main(argv=None) -> int:
             want = None if idx is None else [idx]
         comm_trace = args.comm_trace == "on" or (args.comm_trace == "auto" and world_env > 1)
         dagent.preinit(want, kernel_trace=args.kernel_trace_ready or args.kernel_breakdown, comm_trace=comm_trace)
+    if args.child_started_once:
+        from dynolog_amd import agent as dagent
+        dagent.preinit(None)
 
     import torch
     from dynolog_amd.models.llama import CONFIGS, build_llama, lm_loss
@@ -481,6 +521,14 @@ def main(argv=None) -> int:
                                    comm_init_timeout_ms=int(args.comm_init_timeout_s * 1000),
                                    fault_inject=fault_for_rank(args.agent_fault_inject, env.rank),
                                    pack_mode=args.pack_mode)
+
+    if args.child_started_once:
+        # the agent up and down before the workload: its counting context has
+        # been started (and stopped), no thread or buffer of it remains
+        once = dagent.GpuAgent.start(device=pdist.device_index(env), sample_hz=args.sample_hz, sinks=("memory",),
+                                     pack_mode=args.pack_mode)
+        time.sleep(0.3)
+        once.stop()
 
     # Host CPU PMU co-sampler (one daemon per node, on local rank 0), counting
     # system-wide or, failing that, the ranks of this node.
