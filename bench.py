@@ -121,6 +121,7 @@ def parse_args(argv=None):
                         "carries a few tenths of a percent of process-to-process spread, averaged down")
     p.add_argument("--child-started-once", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-paused-agent", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--child-sampling-agent", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-probe", type=int, default=0,
                    help="instead of the headline: N rounds of no-agent children (plain; agent started and "
                         "stopped before the workload; libdyno_countable.so only), to price a counting "
@@ -158,7 +159,8 @@ _child_seq = [0]  # no-agent children started by this rank (same order on every 
 
 
 def run_baseline_child(args, tag: str, countable: bool = False, started_once: bool = False,
-                       warmup: Optional[int] = None, paused_agent: bool = False) -> dict:
+                       warmup: Optional[int] = None, paused_agent: bool = False,
+                       sampling_agent: bool = False) -> dict:
     """Times the same workload (model, batch, sequence, optimizer, steps) in a
     child process that never loads the agent: no rocprofiler-sdk tool is
     registered, no agent buffers exist.  Under torchrun every rank starts its
@@ -178,6 +180,9 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
         cmd += ["--child-started-once", "--pack-mode", args.pack_mode, "--sample-hz", str(args.sample_hz)]
     if paused_agent:
         cmd += ["--child-started-once", "--child-paused-agent", "--pack-mode", args.pack_mode]
+    if sampling_agent:
+        cmd += ["--child-started-once", "--child-sampling-agent", "--pack-mode", args.pack_mode,
+                "--sample-hz", str(args.sample_hz)]
     env = baseline_child_env(os.environ, _child_seq[0])
     _child_seq[0] += 1
     env.pop("ROCP_TOOL_LIBRARIES", None)
@@ -359,13 +364,14 @@ def run_child_probe(args) -> int:
         if args.child_probe_soak > 0:
             runs.append(run_baseline_child(args, f"soaked{i}", warmup=args.child_probe_soak))
         runs.append(run_baseline_child(args, f"paused_agent{i}", paused_agent=True))
-        print("probe", json.dumps(runs[-5:]), file=sys.stderr, flush=True)
+        runs.append(run_baseline_child(args, f"sampling_agent{i}", sampling_agent=True))
+        print("probe", json.dumps(runs[-6:]), file=sys.stderr, flush=True)
     def mean(kind):
         v = [r["ms_per_step"] for r in runs if "ms_per_step" in r and r["tag"].startswith(kind)]
         return sum(v) / len(v) if v else None
     plain = mean("plain")
     out = {"mode": "child_probe", "rounds": args.child_probe, "runs": runs, "plain_ms_per_step": plain}
-    for kind in ("started_once", "countable", "soaked", "paused_agent"):
+    for kind in ("started_once", "countable", "soaked", "paused_agent", "sampling_agent"):
         m = mean(kind)
         out[kind + "_ms_per_step"] = m
         out[kind + "_vs_plain_pct"] = round((m / plain - 1.0) * 100.0, 3) if m and plain else None
@@ -543,7 +549,7 @@ def main(argv=None) -> int:
         time.sleep(0.3)
         if args.child_paused_agent:
             once.pause()  # stays up, paused, through the workload (its threads and buffers live)
-        else:
+        elif not args.child_sampling_agent:  # else: samples through the workload, never paused
             once.stop()
 
     # Host CPU PMU co-sampler (one daemon per node, on local rank 0), counting
