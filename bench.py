@@ -97,8 +97,10 @@ def parse_args(argv=None):
                         "sampling overhead into GPU kernel time (trainer kernels slower, the agent's own "
                         "kernels) and idle time between kernels -> kernel_breakdown in the result")
     p.add_argument("--skip-baseline", action="store_true")
-    p.add_argument("--pause-settle-steps", type=int, default=2,
-                   help="untimed steps between pausing the samplers and a paused (baseline) window")
+    p.add_argument("--pause-settle-steps", type=int, default=6,
+                   help="untimed steps between pausing the samplers and a paused (baseline) window: "
+                        "right after sampling stops the step stays slower for a while, which biased "
+                        "the pooled A/B low (profiles/round4 g38, g39)")
     p.add_argument("--ab-rounds", type=int, default=6,
                    help="interleaved paused/sampling window pairs for the overhead estimate")
     p.add_argument("--ab-steps", type=int, default=5, help="steps per A/B window")
@@ -637,8 +639,9 @@ def main(argv=None) -> int:
         def settle_paused():
             # A paused window right after sampling still ran slower for a while
             # (profiles/round4/g38: a child sampling through the workload is
-            # +0.52 % against plain children, the pooled A/B read 0.24-0.37 %
-            # with windows started 20 ms after the pause): untimed steps first.
+            # +0.52 % against plain children, while the pooled A/B read
+            # 0.24-0.37 % with windows started 20 ms after the pause; g39: 0, 2
+            # and 6 settle steps gave 0.27 / 0.34 / 0.50 %): untimed steps first.
             for _ in range(args.pause_settle_steps):
                 train_step()
             torch.cuda.synchronize()
