@@ -98,9 +98,8 @@ def parse_args(argv=None):
                         "kernels) and idle time between kernels -> kernel_breakdown in the result")
     p.add_argument("--skip-baseline", action="store_true")
     p.add_argument("--pause-settle-steps", type=int, default=6,
-                   help="untimed steps between pausing the samplers and a paused (baseline) window: "
-                        "right after sampling stops the step stays slower for a while, which biased "
-                        "the pooled A/B low (profiles/round4 g38, g39)")
+                   help="untimed steps between pausing the samplers and a paused (baseline) window "
+                        "(the pooled A/B reads below the child-based overhead, profiles/round4 g38-g40)")
     p.add_argument("--ab-rounds", type=int, default=6,
                    help="interleaved paused/sampling window pairs for the overhead estimate")
     p.add_argument("--ab-steps", type=int, default=5, help="steps per A/B window")
@@ -637,11 +636,12 @@ def main(argv=None) -> int:
         kernel_breakdown = None
 
         def settle_paused():
-            # A paused window right after sampling still ran slower for a while
+            # Paused windows ran slower than processes that never sampled
             # (profiles/round4/g38: a child sampling through the workload is
-            # +0.52 % against plain children, while the pooled A/B read
-            # 0.24-0.37 % with windows started 20 ms after the pause; g39: 0, 2
-            # and 6 settle steps gave 0.27 / 0.34 / 0.50 %): untimed steps first.
+            # +0.52 % against plain children, the pooled A/B 0.24-0.42 %).
+            # Untimed steps after the pause keep the windows away from the last
+            # sampling (g39: 0 / 2 / 6 steps -> 0.27 / 0.34 / 0.50 %; g40: 0.28
+            # with 6, so the gap is not fully explained by this).
             for _ in range(args.pause_settle_steps):
                 train_step()
             torch.cuda.synchronize()
