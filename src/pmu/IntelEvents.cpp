@@ -74,6 +74,27 @@ const AmdEventDef kHswBdw[] = {
     {"cpu", "dtlb_load_misses.walk_completed", "event=0x08,umask=0x0e", "Completed page walks of load DTLB misses"},
     {"cpu", "itlb_misses.walk_completed", "event=0x85,umask=0x0e", "Completed page walks of ITLB misses"},
 };
+// Sandy Bridge / Ivy Bridge (the reference's sandybridge / ivybridge core
+// tables): no L2_RQSTS.MISS / REFERENCES yet, so L2 misses and accesses are
+// summed from the per-type request events
+const AmdEventDef kSnbIvbL2[] = {
+    {"cpu", "l2_rqsts.all_demand_data_rd", "event=0x24,umask=0x03", "Demand data read requests to L2"},
+    {"cpu", "l2_rqsts.demand_data_rd_hit", "event=0x24,umask=0x01", "Demand data reads that hit L2"},
+    {"cpu", "l2_rqsts.all_rfo", "event=0x24,umask=0x0c", "RFO requests to L2"},
+    {"cpu", "l2_rqsts.rfo_miss", "event=0x24,umask=0x08", "RFO requests that missed L2"},
+    {"cpu", "l2_rqsts.all_code_rd", "event=0x24,umask=0x30", "Instruction fetches to L2"},
+    {"cpu", "l2_rqsts.code_rd_miss", "event=0x24,umask=0x20", "Instruction fetches that missed L2"},
+    {"cpu", "l2_rqsts.all_pf", "event=0x24,umask=0xc0", "L2 prefetch requests"},
+    {"cpu", "l2_rqsts.pf_miss", "event=0x24,umask=0x80", "L2 prefetches that missed L2"},
+    {"cpu", "itlb_misses.walk_completed", "event=0x85,umask=0x02", "Completed page walks of ITLB misses"},
+};
+const AmdEventDef kSnbDtlb[] = {
+    {"cpu", "dtlb_load_misses.walk_completed", "event=0x08,umask=0x02", "Completed page walks of load DTLB misses"},
+};
+const AmdEventDef kIvbDtlb[] = {
+    {"cpu", "dtlb_load_misses.walk_completed", "event=0x08,umask=0x82", "Completed page walks of load DTLB misses"},
+};
+
 // Broadwell introduced FP_ARITH_INST_RETIRED (no 512-bit forms before Skylake-SP)
 const AmdEventDef kBdwFp[] = {
     {"cpu", "fp_arith_inst_retired.scalar_double", "event=0xc7,umask=0x01", "Scalar double FP instructions"},
@@ -96,7 +117,8 @@ bool isIntelArch(CpuArch a) {
   return a == CpuArch::IntelGeneric || a == CpuArch::IntelSkylakeX || a == CpuArch::IntelIceLakeX ||
          a == CpuArch::IntelSapphireRapids || a == CpuArch::IntelEmeraldRapids || a == CpuArch::IntelGraniteRapids ||
          a == CpuArch::IntelHaswellX || a == CpuArch::IntelBroadwellX || a == CpuArch::IntelSkylake ||
-         a == CpuArch::IntelIceLake || a == CpuArch::IntelHaswell || a == CpuArch::IntelBroadwell;
+         a == CpuArch::IntelIceLake || a == CpuArch::IntelHaswell || a == CpuArch::IntelBroadwell ||
+         a == CpuArch::IntelSandyBridge || a == CpuArch::IntelIvyBridge;
 }
 
 bool isSprLike(CpuArch a) {
@@ -110,6 +132,12 @@ std::vector<AmdEventDef> intelEventTable(CpuArch arch) {
   if (!isIntelArch(arch)) return v;
   v.insert(v.end(), std::begin(kArch), std::end(kArch));
   if (arch == CpuArch::IntelGeneric) return v;
+  if (arch == CpuArch::IntelSandyBridge || arch == CpuArch::IntelIvyBridge) {
+    v.insert(v.end(), std::begin(kSnbIvbL2), std::end(kSnbIvbL2));
+    if (arch == CpuArch::IntelSandyBridge) v.insert(v.end(), std::begin(kSnbDtlb), std::end(kSnbDtlb));
+    else v.insert(v.end(), std::begin(kIvbDtlb), std::end(kIvbDtlb));
+    return v;
+  }
   if (arch == CpuArch::IntelHaswellX || arch == CpuArch::IntelBroadwellX || arch == CpuArch::IntelHaswell ||
       arch == CpuArch::IntelBroadwell) {
     v.insert(v.end(), std::begin(kHswBdw), std::end(kHswBdw));

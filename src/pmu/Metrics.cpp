@@ -93,7 +93,8 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
     }
     if (ev.count(kIcx) && !ev.count(CpuArch::IntelIceLake)) ev[CpuArch::IntelIceLake] = ev.at(kIcx);
     if (ev.count(kSkx) && (id == "l2_cache_misses" || id == "tlb_misses" || id == "l3_cache_misses_per_instruction"))
-      for (CpuArch a : {CpuArch::IntelHaswellX, CpuArch::IntelBroadwellX, CpuArch::IntelHaswell, CpuArch::IntelBroadwell})
+      for (CpuArch a : {CpuArch::IntelHaswellX, CpuArch::IntelBroadwellX, CpuArch::IntelHaswell, CpuArch::IntelBroadwell,
+                        CpuArch::IntelSandyBridge, CpuArch::IntelIvyBridge})
         if (!ev.count(a)) ev[a] = ev.at(kSkx);
     auto m = std::make_shared<MetricDesc>();
     m->id = std::move(id);
@@ -133,8 +134,22 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
   std::vector<EventRef> l2i = {{"instructions", "instructions"},
                                {"l2_miss", "cpu:l2_rqsts.miss"},
                                {"l2_access", "cpu:l2_rqsts.references"}};
+  // Sandy / Ivy Bridge: misses = demand data reads - their hits + RFO, code
+  // and prefetch misses; accesses = the four request types
+  std::vector<EventRef> l2snb = {{"instructions", "instructions"},
+                                 {"l2_miss", "cpu:l2_rqsts.all_demand_data_rd"},
+                                 {"l2_miss", "cpu:l2_rqsts.demand_data_rd_hit", -1.0},
+                                 {"l2_miss", "cpu:l2_rqsts.rfo_miss"},
+                                 {"l2_miss", "cpu:l2_rqsts.code_rd_miss"},
+                                 {"l2_miss", "cpu:l2_rqsts.pf_miss"},
+                                 {"l2_access", "cpu:l2_rqsts.all_demand_data_rd"},
+                                 {"l2_access", "cpu:l2_rqsts.all_rfo"},
+                                 {"l2_access", "cpu:l2_rqsts.all_code_rd"},
+                                 {"l2_access", "cpu:l2_rqsts.all_pf"}};
   add("l2_cache_misses", "L2 misses (demand IC+DC) per 1k instructions and hit rate",
-      {{kZen4, l2}, {kZen5, l2}, {kSkx, l2i}, {kIcx, l2i}, {kSpr, l2i}}, [](const auto& c, double, double, auto& o) {
+      {{kZen4, l2}, {kZen5, l2}, {kSkx, l2i}, {kIcx, l2i}, {kSpr, l2i}, {CpuArch::IntelSandyBridge, l2snb},
+       {CpuArch::IntelIvyBridge, l2snb}},
+      [](const auto& c, double, double, auto& o) {
         o["l2_mpki"] = ratio(get(c, "l2_miss"), get(c, "instructions")) * 1e3;
         o["l2_hit_rate"] = 1.0 - ratio(get(c, "l2_miss"), get(c, "l2_access"));
       });
@@ -145,7 +160,8 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
                                 {"dtlb_miss", "cpu:dtlb_load_misses.walk_completed"},
                                 {"itlb_miss", "cpu:itlb_misses.walk_completed"}};
   add("tlb_misses", "L1 DTLB / ITLB misses per 1k instructions (Intel: completed page walks)",
-      {{kZen4, tlb}, {kZen5, tlb}, {kSkx, tlbi}, {kIcx, tlbi}, {kSpr, tlbi}},
+      {{kZen4, tlb}, {kZen5, tlb}, {kSkx, tlbi}, {kIcx, tlbi}, {kSpr, tlbi}, {CpuArch::IntelSandyBridge, tlbi},
+       {CpuArch::IntelIvyBridge, tlbi}},
       [](const auto& c, double, double, auto& o) {
         o["dtlb_mpki"] = ratio(get(c, "dtlb_miss"), get(c, "instructions")) * 1e3;
         o["itlb_mpki"] = ratio(get(c, "itlb_miss"), get(c, "instructions")) * 1e3;

@@ -29,6 +29,8 @@ const char* cpuArchName(CpuArch a) {
     case CpuArch::IntelIceLake: return "intel_icl";
     case CpuArch::IntelHaswell: return "intel_hsw";
     case CpuArch::IntelBroadwell: return "intel_bdw";
+    case CpuArch::IntelSandyBridge: return "intel_snb";
+    case CpuArch::IntelIvyBridge: return "intel_ivb";
     default: return "unknown";
   }
 }
@@ -48,6 +50,8 @@ CpuArch makeCpuArch(CpuVendor v, int family, int model) {
     if (family == 6 && (model == 0x7d || model == 0x7e)) return CpuArch::IntelIceLake;
     if (family == 6 && (model == 0x3c || model == 0x45 || model == 0x46)) return CpuArch::IntelHaswell;
     if (family == 6 && (model == 0x3d || model == 0x47)) return CpuArch::IntelBroadwell;
+    if (family == 6 && (model == 0x2a || model == 0x2d)) return CpuArch::IntelSandyBridge;
+    if (family == 6 && (model == 0x3a || model == 0x3e)) return CpuArch::IntelIvyBridge;
     return CpuArch::IntelGeneric;
   }
   if (v != CpuVendor::Amd) return CpuArch::Unknown;

@@ -43,6 +43,8 @@ enum class CpuArch {
   IntelIceLake,         // 0x7d, 0x7e: Ice Lake client (Ice Lake-SP's core encodings)
   IntelHaswell,         // 0x3c, 0x45, 0x46: Haswell client (Haswell-EP's core encodings)
   IntelBroadwell,       // 0x3d, 0x47: Broadwell client (Broadwell-EP's core encodings)
+  IntelSandyBridge,     // 0x2a, 0x2d: Sandy Bridge client / -EP
+  IntelIvyBridge,       // 0x3a, 0x3e: Ivy Bridge client / -EP
 };
 const char* cpuArchName(CpuArch a);
 CpuArch makeCpuArch(CpuVendor v, int family, int model);
