@@ -95,6 +95,14 @@ const AmdEventDef kIvbDtlb[] = {
     {"cpu", "dtlb_load_misses.walk_completed", "event=0x08,umask=0x82", "Completed page walks of load DTLB misses"},
 };
 
+// Nehalem-EX (the reference's nehalemex core table)
+const AmdEventDef kNhmEx[] = {
+    {"cpu", "l2_rqsts.miss", "event=0x24,umask=0xaa", "L2 misses"},
+    {"cpu", "l2_rqsts.references", "event=0x24,umask=0xff", "L2 requests"},
+    {"cpu", "dtlb_load_misses.walk_completed", "event=0x08,umask=0x02", "Completed page walks of load DTLB misses"},
+    {"cpu", "itlb_misses.walk_completed", "event=0x85,umask=0x02", "Completed page walks of ITLB misses"},
+};
+
 // Broadwell introduced FP_ARITH_INST_RETIRED (no 512-bit forms before Skylake-SP)
 const AmdEventDef kBdwFp[] = {
     {"cpu", "fp_arith_inst_retired.scalar_double", "event=0xc7,umask=0x01", "Scalar double FP instructions"},
@@ -118,7 +126,8 @@ bool isIntelArch(CpuArch a) {
          a == CpuArch::IntelSapphireRapids || a == CpuArch::IntelEmeraldRapids || a == CpuArch::IntelGraniteRapids ||
          a == CpuArch::IntelHaswellX || a == CpuArch::IntelBroadwellX || a == CpuArch::IntelSkylake ||
          a == CpuArch::IntelIceLake || a == CpuArch::IntelHaswell || a == CpuArch::IntelBroadwell ||
-         a == CpuArch::IntelSandyBridge || a == CpuArch::IntelIvyBridge;
+         a == CpuArch::IntelSandyBridge || a == CpuArch::IntelIvyBridge || a == CpuArch::IntelNehalemEX ||
+         a == CpuArch::IntelGoldmont || a == CpuArch::IntelSnowRidge || a == CpuArch::IntelKnightsLanding;
 }
 
 bool isSprLike(CpuArch a) {
@@ -131,7 +140,15 @@ std::vector<AmdEventDef> intelEventTable(CpuArch arch) {
   std::vector<AmdEventDef> v;
   if (!isIntelArch(arch)) return v;
   v.insert(v.end(), std::begin(kArch), std::end(kArch));
-  if (arch == CpuArch::IntelGeneric) return v;
+  // Goldmont, Snow Ridge and Knights Landing: the architectural LLC events
+  // count their last-level L2 (l2_cache_misses); nothing else is built in
+  if (arch == CpuArch::IntelGeneric || arch == CpuArch::IntelGoldmont || arch == CpuArch::IntelSnowRidge ||
+      arch == CpuArch::IntelKnightsLanding)
+    return v;
+  if (arch == CpuArch::IntelNehalemEX) {
+    v.insert(v.end(), std::begin(kNhmEx), std::end(kNhmEx));
+    return v;
+  }
   if (arch == CpuArch::IntelSandyBridge || arch == CpuArch::IntelIvyBridge) {
     v.insert(v.end(), std::begin(kSnbIvbL2), std::end(kSnbIvbL2));
     if (arch == CpuArch::IntelSandyBridge) v.insert(v.end(), std::begin(kSnbDtlb), std::end(kSnbDtlb));

@@ -94,7 +94,7 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
     if (ev.count(kIcx) && !ev.count(CpuArch::IntelIceLake)) ev[CpuArch::IntelIceLake] = ev.at(kIcx);
     if (ev.count(kSkx) && (id == "l2_cache_misses" || id == "tlb_misses" || id == "l3_cache_misses_per_instruction"))
       for (CpuArch a : {CpuArch::IntelHaswellX, CpuArch::IntelBroadwellX, CpuArch::IntelHaswell, CpuArch::IntelBroadwell,
-                        CpuArch::IntelSandyBridge, CpuArch::IntelIvyBridge})
+                        CpuArch::IntelSandyBridge, CpuArch::IntelIvyBridge, CpuArch::IntelNehalemEX})
         if (!ev.count(a)) ev[a] = ev.at(kSkx);
     auto m = std::make_shared<MetricDesc>();
     m->id = std::move(id);
@@ -146,9 +146,14 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
                                  {"l2_access", "cpu:l2_rqsts.all_rfo"},
                                  {"l2_access", "cpu:l2_rqsts.all_code_rd"},
                                  {"l2_access", "cpu:l2_rqsts.all_pf"}};
+  // Goldmont / Snow Ridge / Knights Landing: the L2 is the last level
+  std::vector<EventRef> l2llc = {{"instructions", "instructions"},
+                                 {"l2_miss", "cpu:longest_lat_cache.miss"},
+                                 {"l2_access", "cpu:longest_lat_cache.reference"}};
   add("l2_cache_misses", "L2 misses (demand IC+DC) per 1k instructions and hit rate",
       {{kZen4, l2}, {kZen5, l2}, {kSkx, l2i}, {kIcx, l2i}, {kSpr, l2i}, {CpuArch::IntelSandyBridge, l2snb},
-       {CpuArch::IntelIvyBridge, l2snb}},
+       {CpuArch::IntelIvyBridge, l2snb}, {CpuArch::IntelNehalemEX, l2i}, {CpuArch::IntelGoldmont, l2llc},
+       {CpuArch::IntelSnowRidge, l2llc}, {CpuArch::IntelKnightsLanding, l2llc}},
       [](const auto& c, double, double, auto& o) {
         o["l2_mpki"] = ratio(get(c, "l2_miss"), get(c, "instructions")) * 1e3;
         o["l2_hit_rate"] = 1.0 - ratio(get(c, "l2_miss"), get(c, "l2_access"));
@@ -161,7 +166,7 @@ std::shared_ptr<Metrics> makeAvailableMetrics() {
                                 {"itlb_miss", "cpu:itlb_misses.walk_completed"}};
   add("tlb_misses", "L1 DTLB / ITLB misses per 1k instructions (Intel: completed page walks)",
       {{kZen4, tlb}, {kZen5, tlb}, {kSkx, tlbi}, {kIcx, tlbi}, {kSpr, tlbi}, {CpuArch::IntelSandyBridge, tlbi},
-       {CpuArch::IntelIvyBridge, tlbi}},
+       {CpuArch::IntelIvyBridge, tlbi}, {CpuArch::IntelNehalemEX, tlbi}},
       [](const auto& c, double, double, auto& o) {
         o["dtlb_mpki"] = ratio(get(c, "dtlb_miss"), get(c, "instructions")) * 1e3;
         o["itlb_mpki"] = ratio(get(c, "itlb_miss"), get(c, "instructions")) * 1e3;

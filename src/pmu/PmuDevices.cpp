@@ -31,6 +31,10 @@ const char* cpuArchName(CpuArch a) {
     case CpuArch::IntelBroadwell: return "intel_bdw";
     case CpuArch::IntelSandyBridge: return "intel_snb";
     case CpuArch::IntelIvyBridge: return "intel_ivb";
+    case CpuArch::IntelNehalemEX: return "intel_nhm_ex";
+    case CpuArch::IntelGoldmont: return "intel_glm";
+    case CpuArch::IntelSnowRidge: return "intel_snr";
+    case CpuArch::IntelKnightsLanding: return "intel_knl";
     default: return "unknown";
   }
 }
@@ -52,6 +56,10 @@ CpuArch makeCpuArch(CpuVendor v, int family, int model) {
     if (family == 6 && (model == 0x3d || model == 0x47)) return CpuArch::IntelBroadwell;
     if (family == 6 && (model == 0x2a || model == 0x2d)) return CpuArch::IntelSandyBridge;
     if (family == 6 && (model == 0x3a || model == 0x3e)) return CpuArch::IntelIvyBridge;
+    if (family == 6 && model == 0x2e) return CpuArch::IntelNehalemEX;
+    if (family == 6 && (model == 0x5c || model == 0x5f)) return CpuArch::IntelGoldmont;
+    if (family == 6 && model == 0x86) return CpuArch::IntelSnowRidge;
+    if (family == 6 && (model == 0x57 || model == 0x85)) return CpuArch::IntelKnightsLanding;
     return CpuArch::IntelGeneric;
   }
   if (v != CpuVendor::Amd) return CpuArch::Unknown;

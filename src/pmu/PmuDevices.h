@@ -45,6 +45,10 @@ enum class CpuArch {
   IntelBroadwell,       // 0x3d, 0x47: Broadwell client (Broadwell-EP's core encodings)
   IntelSandyBridge,     // 0x2a, 0x2d: Sandy Bridge client / -EP
   IntelIvyBridge,       // 0x3a, 0x3e: Ivy Bridge client / -EP
+  IntelNehalemEX,       // 0x2e: Nehalem-EX
+  IntelGoldmont,        // 0x5c, 0x5f: Goldmont (Apollo Lake, Denverton): the L2 is the last level
+  IntelSnowRidge,       // 0x86: Snow Ridge / Tremont server (L2 last level)
+  IntelKnightsLanding,  // 0x57, 0x85: Knights Landing / Mill (L2 last level)
 };
 const char* cpuArchName(CpuArch a);
 CpuArch makeCpuArch(CpuVendor v, int family, int model);
