@@ -125,6 +125,7 @@ def parse_args(argv=None):
     p.add_argument("--child-started-once", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-paused-agent", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-sampling-agent", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--child-kernel-breakdown", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-probe", type=int, default=0,
                    help="instead of the headline: N rounds of no-agent children (plain; agent started and "
                         "stopped before the workload; libdyno_countable.so only), to price a counting "
@@ -186,6 +187,10 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
     if sampling_agent:
         cmd += ["--child-started-once", "--child-sampling-agent", "--pack-mode", args.pack_mode,
                 "--sample-hz", str(args.sample_hz)]
+    if getattr(args, "kernel_breakdown", False) and not countable:
+        # the no-agent child traces its own kernels too (a kernel-tracing tool only,
+        # no counting context started): the paused windows' kernels against them
+        cmd += ["--child-kernel-breakdown"]
     env = baseline_child_env(os.environ, _child_seq[0])
     _child_seq[0] += 1
     env.pop("ROCP_TOOL_LIBRARIES", None)
@@ -202,7 +207,10 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
             res["started_once"] = True
         if r.returncode == 0 and os.path.getsize(path) > 0:
             with open(path) as f:
-                res["ms_per_step"] = json.loads(f.read())["ms_per_step"]
+                child_out = json.loads(f.read())
+                res["ms_per_step"] = child_out["ms_per_step"]
+                if "kernel_breakdown" in child_out:
+                    res["kernel_breakdown"] = child_out["kernel_breakdown"]
         return res
     except Exception as e:  # noqa: BLE001 - the baseline is extra information
         return {"tag": tag, "error": str(e)}
@@ -354,7 +362,13 @@ def summarize_kernel_windows(kwin: dict, steps: int) -> dict:
            "trainer_kernel_delta_ms_per_step": r(sum(d for d, _ in deltas)),
            "top_slower_kernels": [{"name": nm[:120], "delta_ms_per_step": r(d),
                                    "paused_ms_per_step": r(kp.get(nm, (0.0, 0))[0])} for d, nm in deltas[:8]],
-           "top_faster_kernels": [{"name": nm[:120], "delta_ms_per_step": r(d)} for d, nm in deltas[-4:]]}
+           "top_faster_kernels": [{"name": nm[:120], "delta_ms_per_step": r(d)} for d, nm in deltas[-4:]],
+           # the largest kernels' own time per step in each kind of window
+           "top_kernels_ms_per_step": [{"name": nm[:120], "active": r(ka.get(nm, (0.0, 0))[0]),
+                                        "paused": r(kp.get(nm, (0.0, 0))[0])}
+                                       for nm in sorted(set(ka) | set(kp),
+                                                        key=lambda n: -max(ka.get(n, (0.0, 0))[0],
+                                                                           kp.get(n, (0.0, 0))[0]))[:8]]}
     return out
 
 
@@ -505,6 +519,9 @@ def main(argv=None) -> int:
     if args.child_started_once:
         from dynolog_amd import agent as dagent
         dagent.preinit(None)
+    elif args.child_kernel_breakdown:
+        from dynolog_amd import agent as dagent
+        dagent.preinit(None, kernel_trace=True)
 
     import torch
     from dynolog_amd.models.llama import CONFIGS, build_llama, lm_loss
@@ -655,7 +672,15 @@ def main(argv=None) -> int:
                 train_step()
             torch.cuda.synchronize()
 
-        meas_s, m0, m1 = timed(args.steps)
+        if args.child_kernel_breakdown:
+            # a no-agent child: the headline window with its kernels traced
+            kt = dagent.KernelTrace().start()
+            meas_s, m0, m1 = timed(args.steps)
+            kt.stop()
+            kernel_breakdown = summarize_kernel_windows({"active": [kt.summary(top=100000)],
+                                                         "paused": [kt.summary(top=100000)]}, args.steps)
+        else:
+            meas_s, m0, m1 = timed(args.steps)
         # per-rank time to finish its own steps inside the headline window
         # (stragglers / imbalance show here; the window itself ends at the barrier),
         # and every rank's window on its own CLOCK_MONOTONIC: samples carry their
