@@ -922,6 +922,21 @@ bool Agent::step(hipStream_t stream, std::string* err) {
   // stream never waits on the (lowest-priority) pack stream.  A pack still
   // queued behind the step's own kernels is picked up by the next step.
   const uint64_t head = completedPackHead();
+  if (hostPack_ && !collective_) {
+    // host packing, world 1 / shm mailbox: the gather is a copy on this (the
+    // trainer's) thread with no GPU work, so its cost is host time, and no
+    // timing events go onto the trainer's stream
+    const uint64_t t0 = monoNs();
+    const bool ok = gatherLocal(stream, head, err);
+    const uint64_t ns = monoNs() - t0;
+    gatherTimed_++;
+    gatherLatSumNs_ += ns;
+    gatherLatLastNs_ = ns;
+    uint64_t mx = gatherLatMaxNs_.load();
+    while (ns > mx && !gatherLatMaxNs_.compare_exchange_weak(mx, ns)) {
+    }
+    return ok;
+  }
   harvestGatherTimers();
   const int timer = beginGatherTimer(stream);
   const bool ok = collective_ ? gatherCollective(stream, head, err) : gatherLocal(stream, head, err);
