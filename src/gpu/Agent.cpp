@@ -988,13 +988,8 @@ void Agent::hostGatherBlock(uint8_t* dst, const GatherRange& rg, uint64_t head, 
   gh->device = cfg_.device;
   gh->pci_loc = pciLoc_;
   gh->reserved = 0;
-  auto* out = reinterpret_cast<DynoSlot*>(dst + sizeof(DynoGatherHeader));
-  const uint64_t mask = cfg_.ringSlots - 1;
-  // the range wraps the ring at most once
-  const uint64_t a = rg.first & mask;
-  const uint64_t n1 = std::min<uint64_t>(rg.count, cfg_.ringSlots - a);
-  memcpy(out, hRing_ + a, n1 * sizeof(DynoSlot));
-  if (n1 < rg.count) memcpy(out + n1, hRing_, (rg.count - n1) * sizeof(DynoSlot));
+  copyRingRange(reinterpret_cast<DynoSlot*>(dst + sizeof(DynoGatherHeader)), hRing_, cfg_.ringSlots, rg.first,
+                rg.count);
 }
 
 // world 1, or the shm mailbox: gather_prep straight into a drain buffer (or

@@ -905,3 +905,20 @@ TEST(GpuHost, SetsSharingAPassKeepTheirOwnMetrics) {
   agg.logInterval(ml, 0.001, 1'017'000'000ull);
   EXPECT_NEAR(std::stod(store->records.back().at("hbm_read_gbps").asString()), 1000.0, 1e-3);
 }
+
+// Host packing's gather copy: a range that wraps the ring comes out in
+// sequence order, a range at the start of the ring unchanged.
+TEST(GpuHost, CopyRingRangeWrapsOnce) {
+  constexpr uint64_t kCap = 16;
+  std::vector<DynoSlot> ring(kCap);
+  for (uint64_t i = 0; i < kCap; ++i) ring[i].seq = 0;
+  for (uint64_t seq = 20; seq < 36; ++seq) ring[seq & (kCap - 1)].seq = seq;  // slots 20..35
+  std::vector<DynoSlot> out(kCap);
+  EXPECT_EQ(copyRingRange(out.data(), ring.data(), kCap, 26, 9), 9u);  // 26..34 wraps at 32
+  for (uint32_t i = 0; i < 9; ++i) EXPECT_EQ(out[i].seq, 26u + i);
+  EXPECT_EQ(copyRingRange(out.data(), ring.data(), kCap, 32, 4), 4u);
+  for (uint32_t i = 0; i < 4; ++i) EXPECT_EQ(out[i].seq, 32u + i);
+  EXPECT_EQ(copyRingRange(out.data(), ring.data(), kCap, 20, 0), 0u);
+  EXPECT_EQ(copyRingRange(out.data(), ring.data(), kCap, 20, 99), 16u);  // never more than the ring
+  for (uint32_t i = 0; i < 16; ++i) EXPECT_EQ(out[i].seq, 20u + i);
+}
