@@ -126,6 +126,10 @@ def parse_args(argv=None):
     p.add_argument("--child-paused-agent", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-sampling-agent", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-kernel-breakdown", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--child-agent-unpinned", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--child-probe-unpinned", action="store_true",
+                   help="child probe: also a sampling child whose agent threads are not pinned to the "
+                        "GPU's NUMA-local CPUs")
     p.add_argument("--child-probe", type=int, default=0,
                    help="instead of the headline: N rounds of no-agent children (plain; agent started and "
                         "stopped before the workload; libdyno_countable.so only), to price a counting "
@@ -164,7 +168,7 @@ _child_seq = [0]  # no-agent children started by this rank (same order on every 
 
 def run_baseline_child(args, tag: str, countable: bool = False, started_once: bool = False,
                        warmup: Optional[int] = None, paused_agent: bool = False,
-                       sampling_agent: bool = False) -> dict:
+                       sampling_agent: bool = False, unpinned: bool = False) -> dict:
     """Times the same workload (model, batch, sequence, optimizer, steps) in a
     child process that never loads the agent: no rocprofiler-sdk tool is
     registered, no agent buffers exist.  Under torchrun every rank starts its
@@ -187,6 +191,8 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
     if sampling_agent:
         cmd += ["--child-started-once", "--child-sampling-agent", "--pack-mode", args.pack_mode,
                 "--sample-hz", str(args.sample_hz)]
+        if unpinned:
+            cmd += ["--child-agent-unpinned"]
     if getattr(args, "kernel_breakdown", False) and not countable:
         # the no-agent child traces its own kernels too (a kernel-tracing tool only,
         # no counting context started): the paused windows' kernels against them
@@ -385,13 +391,15 @@ def run_child_probe(args) -> int:
             runs.append(run_baseline_child(args, f"soaked{i}", warmup=args.child_probe_soak))
         runs.append(run_baseline_child(args, f"paused_agent{i}", paused_agent=True))
         runs.append(run_baseline_child(args, f"sampling_agent{i}", sampling_agent=True))
-        print("probe", json.dumps(runs[-6:]), file=sys.stderr, flush=True)
+        if args.child_probe_unpinned:
+            runs.append(run_baseline_child(args, f"sampling_unpinned{i}", sampling_agent=True, unpinned=True))
+        print("probe", json.dumps(runs[-7:]), file=sys.stderr, flush=True)
     def mean(kind):
         v = [r["ms_per_step"] for r in runs if "ms_per_step" in r and r["tag"].startswith(kind)]
         return sum(v) / len(v) if v else None
     plain = mean("plain")
     out = {"mode": "child_probe", "rounds": args.child_probe, "runs": runs, "plain_ms_per_step": plain}
-    for kind in ("started_once", "countable", "soaked", "paused_agent", "sampling_agent"):
+    for kind in ("started_once", "countable", "soaked", "paused_agent", "sampling_agent", "sampling_unpinned"):
         m = mean(kind)
         out[kind + "_ms_per_step"] = m
         out[kind + "_vs_plain_pct"] = round((m / plain - 1.0) * 100.0, 3) if m and plain else None
@@ -570,7 +578,7 @@ def main(argv=None) -> int:
         # the agent up and down before the workload: its counting context has
         # been started (and stopped), no thread or buffer of it remains
         once = dagent.GpuAgent.start(device=pdist.device_index(env), sample_hz=args.sample_hz, sinks=("memory",),
-                                     pack_mode=args.pack_mode)
+                                     pack_mode=args.pack_mode, pin_threads=not args.child_agent_unpinned)
         time.sleep(0.3)
         if args.child_paused_agent:
             once.pause()  # stays up, paused, through the workload (its threads and buffers live)

@@ -421,7 +421,8 @@ class GpuAgent:
               slot_ring: str = "", stages: int = 64,
               force_collective: bool = False, counter_passes: str = "",
               gather_scope: str = "node", force_collective_role: str = "",
-              comm_init_timeout_ms: int = 60000, pack_mode: str = "host") -> "GpuAgent":
+              comm_init_timeout_ms: int = 60000, pack_mode: str = "host",
+              pin_threads: bool = True) -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
@@ -491,7 +492,8 @@ class GpuAgent:
                    ring_slots=ring_slots, gather_cap_slots=cap,
                    gather_mode=gather_mode, counter_set=counter_set, log_interval_ms=log_interval_ms,
                    sinks=list(sinks), log_file=log_file, daemon_endpoint=daemon_endpoint,
-                   comm_init_timeout_ms=int(comm_init_timeout_ms), pack_mode=pack_mode)
+                   comm_init_timeout_ms=int(comm_init_timeout_ms), pack_mode=pack_mode,
+                   pin_threads=bool(pin_threads))
         if counter_passes:
             cfg["counter_passes"] = counter_passes
         if labels is not None:
