@@ -226,13 +226,18 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
         r = subprocess.Popen(cmd, env=env, stdout=sys.stderr)
         seen = None
         if daemon is not None:
-            # what the daemon reads while the job runs (its counter visibility and rate)
-            while r.poll() is None and time.time() - t0 < 20.0:
+            # what the daemon reads while the job runs (its counter visibility and
+            # rate): the last answer taken with the job still running
+            next_probe = t0 + 3.0
+            while r.poll() is None and time.time() - t0 < 600.0:
+                if time.time() >= next_probe:
+                    mon = daemon.rpc({"fn": "getGpuCounterMonitor"}) or {}
+                    view = [{k: g.get(k) for k in ("sampling", "counter_visibility", "sample_hz")}
+                            for g in mon.get("gpus", [])][:1]
+                    if r.poll() is None:
+                        seen = view
+                    next_probe = time.time() + 2.0
                 time.sleep(0.2)
-            if r.poll() is None:
-                mon = daemon.rpc({"fn": "getGpuCounterMonitor"}) or {}
-                seen = [{k: g.get(k) for k in ("sampling", "counter_visibility", "sample_hz")}
-                        for g in mon.get("gpus", [])][:1]
         try:
             r.wait(timeout=600)
         except subprocess.TimeoutExpired:

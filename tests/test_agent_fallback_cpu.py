@@ -175,6 +175,72 @@ def test_baseline_child_env_hosts_its_own_store():
     assert one["MASTER_PORT"] == "29500" and "TORCHELASTIC_USE_AGENT_STORE" not in one
 
 
+def test_daemon_sampled_child_is_countable_and_stops_its_daemon(monkeypatch):
+    """--child-probe-daemon: the child runs with libdyno_countable.so while a
+    daemon samples its GPU (lite set, the probe's rate) and is stopped after;
+    the daemon's view mid-run is recorded with the child's time."""
+    import importlib.util
+    import json as _json
+    import subprocess
+    import types
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    from dynolog_amd import _native
+    from dynolog_amd.utils import daemon as dmod
+    seen = {}
+
+    class FakeDaemon:
+        def __init__(self, args):
+            seen["daemon_args"] = list(args)
+        def start(self):
+            seen["started"] = True
+            return self
+        def rpc(self, req):
+            return {"gpus": [{"sampling": True, "counter_visibility": "full", "sample_hz": 1000.0}]}
+        def stop(self):
+            seen["stopped"] = True
+            return 0
+
+    class FakeChild:
+        def __init__(self, cmd, env=None, stdout=None):
+            seen["env_tool"] = env.get("ROCP_TOOL_LIBRARIES")
+            self.path = cmd[cmd.index("--json-out") + 1]
+            self.polls = 0
+            self.returncode = None
+        def poll(self):
+            self.polls += 1
+            if self.polls > 40:
+                with open(self.path, "w") as f:
+                    f.write(_json.dumps({"ms_per_step": 338.5}))
+                self.returncode = 0
+            return self.returncode
+        def wait(self, timeout=None):
+            while self.poll() is None:
+                pass
+            return self.returncode
+        def kill(self):
+            pass
+
+    monkeypatch.setattr(dmod, "DaemonProcess", FakeDaemon)
+    monkeypatch.setattr(subprocess, "Popen", FakeChild)
+    clock = [1000.0]  # fake time: each 0.2 s poll interval advances it
+
+    def fake_sleep(sec):
+        clock[0] += sec
+    monkeypatch.setattr(b.time, "time", lambda: clock[0])
+    monkeypatch.setattr(b.time, "sleep", fake_sleep)
+    args = types.SimpleNamespace(steps=5, warmup=2, model="llama3-8b", micro_batch=2, seq_len=4096,
+                                 optimizer="adamw", batches=1, pack_mode="host", sample_hz=1000.0)
+    res = b.run_baseline_child(args, "daemon_sampling0", daemon_hz=1000.0)
+    assert res["ms_per_step"] == 338.5 and res["countable"] is True
+    assert seen["env_tool"] == _native.COUNTABLE_LIB
+    assert "--gpu_counters=lite" in seen["daemon_args"] and "--gpu_counter_hz=1000.0" in seen["daemon_args"]
+    assert seen["started"] and seen["stopped"]
+    assert res["daemon_while_job_ran"] == [{"sampling": True, "counter_visibility": "full", "sample_hz": 1000.0}]
+
+
 _PARENT = r"""
 import importlib.util, os, subprocess, sys
 import torch.distributed as dist
