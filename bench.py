@@ -229,12 +229,19 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
             # what the daemon reads while the job runs (its counter visibility and
             # rate): the last answer taken with the job still running
             next_probe = t0 + 3.0
+            first = None  # (time, samples) of the first in-job answer: the achieved rate
             while r.poll() is None and time.time() - t0 < 600.0:
                 if time.time() >= next_probe:
                     mon = daemon.rpc({"fn": "getGpuCounterMonitor"}) or {}
-                    view = [{k: g.get(k) for k in ("sampling", "counter_visibility", "sample_hz")}
-                            for g in mon.get("gpus", [])][:1]
+                    now = time.time()
+                    g0 = (mon.get("gpus") or [{}])[0]
+                    view = {"counter_visibility": g0.get("counter_visibility"), "samples": g0.get("samples"),
+                            "sample_hz": mon.get("sample_hz"), "compute_pids": g0.get("compute_pids")}
                     if r.poll() is None:
+                        if first is None:
+                            first = (now, view["samples"] or 0)
+                        elif now > first[0]:
+                            view["achieved_hz"] = round(((view["samples"] or 0) - first[1]) / (now - first[0]), 1)
                         seen = view
                     next_probe = time.time() + 2.0
                 time.sleep(0.2)

@@ -198,7 +198,9 @@ def test_daemon_sampled_child_is_countable_and_stops_its_daemon(monkeypatch):
             seen["started"] = True
             return self
         def rpc(self, req):
-            return {"gpus": [{"sampling": True, "counter_visibility": "full", "sample_hz": 1000.0}]}
+            seen["rpcs"] = seen.get("rpcs", 0) + 1
+            return {"sample_hz": 1000.0, "gpus": [{"counter_visibility": "full", "compute_pids": [7],
+                                                   "samples": 2000 * seen["rpcs"]}]}
         def stop(self):
             seen["stopped"] = True
             return 0
@@ -238,7 +240,9 @@ def test_daemon_sampled_child_is_countable_and_stops_its_daemon(monkeypatch):
     assert seen["env_tool"] == _native.COUNTABLE_LIB
     assert "--gpu_counters=lite" in seen["daemon_args"] and "--gpu_counter_hz=1000.0" in seen["daemon_args"]
     assert seen["started"] and seen["stopped"]
-    assert res["daemon_while_job_ran"] == [{"sampling": True, "counter_visibility": "full", "sample_hz": 1000.0}]
+    v = res["daemon_while_job_ran"]  # probes 2 s apart, 2000 samples apart
+    assert v["counter_visibility"] == "full" and v["sample_hz"] == 1000.0 and v["compute_pids"] == [7]
+    assert abs(v["achieved_hz"] - 1000.0) < 1.0
 
 
 _PARENT = r"""
