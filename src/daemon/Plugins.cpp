@@ -134,18 +134,25 @@ struct AgentRec {
 };
 std::map<std::string, AgentRec> gAgentRecs;  // "bdf:<x>" or "dev:<n>" -> newest
 
-std::vector<std::string> recordKeys(const Json& rec) {
-  std::vector<std::string> k;
-  if (rec.contains("gpu_bdf") && rec.at("gpu_bdf").isString()) k.push_back("bdf:" + rec.at("gpu_bdf").asString());
-  if (rec.contains("device") && rec.at("device").isNumber()) k.push_back("dev:" + std::to_string(rec.at("device").asInt()));
-  return k;
+// The one key a record is filed and found under: its GPU's PCI location
+// when it carries one, the device index only when it does not.  The two
+// never mix: an agent's "device" is its process's HIP index (0 under
+// HIP_VISIBLE_DEVICES on every GPU) while the daemon's is the rocprofiler
+// agent index, so a device-index match across them names the wrong GPU.
+std::string recordKey(const Json& rec) {
+  if (rec.contains("gpu_bdf") && rec.at("gpu_bdf").isString() && !rec.at("gpu_bdf").asString().empty())
+    return "bdf:" + rec.at("gpu_bdf").asString();
+  if (rec.contains("device") && rec.at("device").isNumber()) return "dev:" + std::to_string(rec.at("device").asInt());
+  return "";
 }
 }  // namespace
 
 void noteAgentGpuRecord(const Json& rec, uint64_t nowMs) {
   if (!rec.isObject() || rec.contains("phase")) return;  // per-phase records are not per-GPU totals
+  const std::string k = recordKey(rec);
+  if (k.empty()) return;
   std::lock_guard<std::mutex> g(gAgentRecMu);
-  for (const auto& k : recordKeys(rec)) gAgentRecs[k] = AgentRec{rec, nowMs};
+  gAgentRecs[k] = AgentRec{rec, nowMs};
 }
 
 int fillFromAgentRecord(Json& rec, uint64_t nowMs, uint64_t maxAgeMs) {
@@ -153,14 +160,8 @@ int fillFromAgentRecord(Json& rec, uint64_t nowMs, uint64_t maxAgeMs) {
   AgentRec a;
   {
     std::lock_guard<std::mutex> g(gAgentRecMu);
-    // the GPU's PCI location first: device indices differ between processes
-    for (const auto& k : recordKeys(rec)) {
-      auto it = gAgentRecs.find(k);
-      if (it != gAgentRecs.end() && nowMs - it->second.ms <= maxAgeMs) {
-        a = it->second;
-        break;
-      }
-    }
+    auto it = gAgentRecs.find(recordKey(rec));
+    if (it != gAgentRecs.end() && nowMs - it->second.ms <= maxAgeMs) a = it->second;
   }
   if (!a.rec.isObject()) return 0;
   std::string filled, still;

@@ -210,6 +210,12 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     *err = "an earlier stop() left a GPU agent thread stuck in the runtime; restart the process";
     return false;
   }
+  if (samplerHold_) {
+    // an on-demand capture (SQTT / dispatch counting, Python API) still
+    // programs the SQ: a new counting context now could hang both
+    *err = "an on-demand capture still holds the counter sampler; finish it before start()";
+    return false;
+  }
   if (cfg.world < 1 || cfg.rank < 0 || cfg.rank >= cfg.world ||
       (!cfg.rankLabels.empty() && static_cast<int>(cfg.rankLabels.size()) != cfg.world)) {
     *err = "bad gather group: rank " + std::to_string(cfg.rank) + " of " + std::to_string(cfg.world) + " with " +
@@ -579,7 +585,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   // must not be overwritten when the thread comes up
   setSampleHz(cfg_.sampleHz);
   samplerDone_ = consumerDone_ = ctlDone_ = false;
-  samplerParked_ = false;
+  parkedGen_ = holdGen_.load();  // no hold is pending (start() refuses while one is held)
   samplerThread_ = std::thread([this] {
     samplerLoop();
     samplerDone_ = true;
@@ -770,13 +776,13 @@ void Agent::samplerLoop() {
         sampler_->stop();
         wasPaused = true;
       }
-      samplerParked_.store(true, std::memory_order_release);  // holdSampler() waits for this
+      // holdSampler() waits for its generation: the context is stopped now
+      parkedGen_.store(holdGen_.load(), std::memory_order_release);
       usleep(2000);
       next = monoNs();
       continue;
     }
     if (wasPaused) {
-      samplerParked_.store(false, std::memory_order_release);
       sampler_->select();
       if (!sampler_->start(&err)) {
         lastError_ = err;
@@ -1391,15 +1397,20 @@ int Agent::ncclSettle(int result, uint64_t timeoutNs) {
 
 void Agent::pause() { paused_ = true; }
 bool Agent::holdSampler() {
+  // A generation per hold: the loop acknowledges the generation it parked
+  // under, so a release followed at once by another hold waits for the loop
+  // to park AGAIN (it may be restarting its context for the gap between them)
+  // instead of returning on the previous hold's stale "parked".
+  const uint64_t gen = holdGen_.fetch_add(1) + 1;
   if (samplerHold_.exchange(true)) return false;
   // A capture programs the same counters: it may start only once the sampler
   // loop has stopped its device-counting context (a read still in flight
   // when another counting context starts can wait forever).  Normally ~1 ms.
   const uint64_t deadline = monoNs() + 2'000'000'000ull;
-  while (running_ && samplerThread_.joinable() && !samplerParked_.load(std::memory_order_acquire) &&
+  while (running_ && samplerThread_.joinable() && parkedGen_.load(std::memory_order_acquire) < gen &&
          monoNs() < deadline)
     usleep(200);
-  if (running_ && !samplerParked_.load())
+  if (running_ && samplerThread_.joinable() && parkedGen_.load() < gen)
     LOG(WARNING) << "GPU agent: the sampler did not park within 2 s for an on-demand capture";
   return true;
 }
@@ -1592,7 +1603,8 @@ Json Agent::dispatchCountersRequest(const Json& req, Json res) {
       }
     res["dispatches"] = d;
   }
-  if (holdHere) releaseSampler();
+  // persistent mode keeps its context started: the sampler stays held
+  if (holdHere && !dc.keepsSqProgrammed()) releaseSampler();
   return res;
 }
 

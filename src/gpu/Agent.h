@@ -195,7 +195,9 @@ class Agent {
   // thread); unlike paused_ it never gates step(), so a rank in a collective
   // gather keeps issuing its gathers while it is being captured.
   std::atomic<bool> samplerHold_{false};
-  std::atomic<bool> samplerParked_{false};  // the sampler loop is paused / held with its context stopped
+  // holdSampler() generations: holdGen_ counts holds, parkedGen_ is the
+  // newest generation the sampler loop parked under (its context stopped)
+  std::atomic<uint64_t> holdGen_{0}, parkedGen_{0};
   uint64_t pciLoc_ = 0;  // this rank's GPU (DynoGatherHeader::pci_loc)
   // The agent's communicator is non-blocking (init can be abandoned at a
   // deadline): wait for a call that returned ncclInProgress to finish.

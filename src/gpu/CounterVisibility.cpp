@@ -50,6 +50,16 @@ unsigned crossProcessVisibleMask(const std::vector<std::string>& names) {
   return m;
 }
 
+bool visibilityTableMeasuredFor(const std::string& arch) { return arch == "gfx950"; }
+
+unsigned crossProcessVisibleMask(const std::vector<std::string>& names, const std::string& arch) {
+  if (visibilityTableMeasuredFor(arch)) return crossProcessVisibleMask(names);
+  unsigned m = 0;
+  for (size_t i = 0; i < names.size() && i < 32; ++i)
+    if (names[i].rfind("GRBM_", 0) == 0) m |= 1u << i;
+  return m;
+}
+
 std::map<uint64_t, std::set<int>> kfdProcessesByGpu(const std::string& kfdRoot) {
   std::map<uint64_t, std::set<int>> out;
   const std::string procDir = kfdRoot + "/proc";

@@ -40,6 +40,13 @@ bool crossProcessVisible(const std::string& counter);
 // bits of a pass's delta[] positions (its names; "" = unused) whose counter
 // is in that group
 unsigned crossProcessVisibleMask(const std::vector<std::string>& names);
+// The same for a GPU of architecture `arch` (rocprofiler agent name): the
+// group above was measured on gfx950 only (profiles/round4/g02), so on any
+// other target only the GRBM_* clocks, which count the whole GPU on every
+// gfx9 part, are taken as readable for other processes; every SQ / TCC / TA
+// counter of an uncountable job is then reported unavailable, never guessed.
+unsigned crossProcessVisibleMask(const std::vector<std::string>& names, const std::string& arch);
+bool visibilityTableMeasuredFor(const std::string& arch);
 
 // KFD's per-process queues: gpu_id (KFD identifier, AgentInfo::gpu_id) ->
 // pids with at least one queue on that GPU.  kfdRoot is /sys/class/kfd/kfd

@@ -68,6 +68,7 @@ class DeviceMonitor {
     int index = 0;
     uint64_t gpuId = 0;   // KFD id (CounterVisibility: which processes run on it)
     uint64_t pciLoc = 0;  // DynoGatherHeader::pci_loc of the records
+    std::string arch;     // agent name (gfx950): which visibility table applies
     std::vector<Pass> passes;
     std::unique_ptr<Pass> alt;  // "auto": the readable-only set used while limited
     bool onAlt = false;

@@ -88,6 +88,13 @@ class DispatchCounters {
   };
   bool arm(const DispatchCountersRequest& req, std::string* err);
   bool buildConfigs(const std::vector<std::string>& names, std::string* err);
+ public:
+  // The counting context stays started after finish() (persistent mode, after
+  // the first capture): a holder of the agent's sampler must keep it held,
+  // or the device-counting sampler and this context program the SQ together.
+  bool keepsSqProgrammed() const { return persistent_ && ctxStarted_; }
+
+ private:
   static int slotOfRecord(AgentCfg& a, uint64_t recordId);
 
   mutable std::mutex mu_;

@@ -232,6 +232,17 @@ Json KernelTracer::summary(size_t topN) const {
   Json j = Json::object();
   const uint64_t window = windowEnd_ > windowStart_ ? windowEnd_ - windowStart_ : 0;
   j["window_ms"] = window * 1e-6;
+  // Window bounds and the first / last dispatch of it (CLOCK_MONOTONIC ns):
+  // a short capture then tells an idle process (dispatches bunched at one
+  // end, or none near the start) from records the tracer lost.
+  j["window_start_ns"] = static_cast<unsigned long long>(windowStart_);
+  j["window_end_ns"] = static_cast<unsigned long long>(windowEnd_);
+  if (!iv.empty()) {
+    uint64_t lastEnd = 0;
+    for (const auto& [s, e] : iv) lastEnd = std::max(lastEnd, e);
+    j["first_dispatch_start_ns"] = static_cast<unsigned long long>(iv.front().first);
+    j["last_dispatch_end_ns"] = static_cast<unsigned long long>(lastEnd);
+  }
   j["dispatches"] = static_cast<unsigned long long>(recs.size());
   j["distinct_kernels"] = static_cast<unsigned long long>(by.size());
   j["kernel_time_ms"] = total * 1e-6;

@@ -52,8 +52,9 @@ def _run(native_built, tmp_path, sockdir, switches=()):
     with DaemonProcess(["--enable_ipc_monitor"], env=env) as d:
         script = textwrap.dedent("""
             import os, time, torch
-            print("PID", os.getpid(), flush=True)
             x = torch.randn(128, 128)
+            y = x @ x   # warm before reporting ready
+            print("PID", os.getpid(), flush=True)
             t0 = time.time()
             while time.time() - t0 < 40:
                 for _ in range(50):
