@@ -144,6 +144,39 @@ class RecordLogger : public Logger {
 
 // Thread-safe in-memory sink. Each finalize() appends one record
 // {"ts_ms": ..., <keys>...}; bounded by capacity (oldest dropped).
+// Records the Logger calls of one or more records for replay into another
+// Logger later, on another thread: a producer that must not block (the GPU
+// agent's consumer aggregates under its lock) hands the records to a thread
+// that feeds the real sinks, so a stalled sink (a full stderr pipe, a slow
+// HTTP endpoint, an absent daemon) never stalls ingestion or training.
+class RecordingLogger : public Logger {
+ public:
+  struct Op {
+    enum Kind : uint8_t { kTs, kInt, kUint, kFloat, kStr, kFinalize } kind;
+    std::string key;
+    int64_t i = 0;
+    uint64_t u = 0;
+    float f = 0.f;
+    std::string s;
+    Timestamp ts{};
+  };
+  void setTimestamp(Timestamp ts = std::chrono::system_clock::now()) override { ops_.push_back(Op{Op::kTs, {}, 0, 0, 0.f, {}, ts}); }
+  void logInt(const std::string& key, int64_t val) override { ops_.push_back(Op{Op::kInt, key, val, 0, 0.f, {}, {}}); }
+  void logFloat(const std::string& key, float val) override { ops_.push_back(Op{Op::kFloat, key, 0, 0, val, {}, {}}); }
+  void logUint(const std::string& key, uint64_t val) override { ops_.push_back(Op{Op::kUint, key, 0, val, 0.f, {}, {}}); }
+  void logStr(const std::string& key, const std::string& val) override {
+    ops_.push_back(Op{Op::kStr, key, 0, 0, 0.f, val, {}});
+  }
+  void finalize() override { ops_.push_back(Op{Op::kFinalize, {}, 0, 0, 0.f, {}, {}}); }
+  bool empty() const { return ops_.empty(); }
+  std::vector<Op> take() { return std::move(ops_); }
+  // the recorded calls, in order, into `to`
+  static void replay(const std::vector<Op>& ops, Logger& to);
+
+ private:
+  std::vector<Op> ops_;
+};
+
 class MemoryLogger : public JsonLogger {
  public:
   struct Store {

@@ -62,7 +62,7 @@ def test_dispatch_counters_gemm_and_copy(native_built):
     p = prec["dispatches"][0]["derived"]
     assert "fp32_active" in p and p["mfma_bf16_tflops"] > 100, prec
     assert st["samples_failed"] == 0
-    assert st["dispatch_counting_started"] is True and st["pack_mode"] == "host", st
+    assert st["dispatch_counting_started"] is True and st["pack_mode"] == "step", st
 
 
 def test_reduced_rate_hbm_pass_matches_dispatch_counting(native_built):
