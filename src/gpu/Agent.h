@@ -38,6 +38,7 @@
 #include "gpu/GatherPlan.h"
 #include "gpu/RocprofSampler.h"
 #include "gpu/SlotAggregator.h"
+#include "gpu/SlotBroadcast.h"
 #include "gpu/SlotFormat.h"
 #include "ring/RingBuffer.h"
 #include "sinks/Logger.h"
@@ -80,6 +81,15 @@ struct AgentConfig {
   //          HBM ring: its copies ran as blit kernels beside the trainer's GEMMs
   //          (profiles/round4/g04b)
   std::string packMode = "step";
+  // Who reads the counters:
+  //   agent  (default) this process: its sampler thread drives rocprofiler-sdk device
+  //          counting for its GPU
+  //   daemon the node's dynolog daemon (--enable_gpu_counters, per-GPU threads): the
+  //          agent takes its slots from the daemon's node-local broadcast ring
+  //          (SlotBroadcast.h) and tags, packs (pack_mode step), gathers and logs them
+  //          exactly as its own -- a sidecar: no counting context runs in the job
+  std::string sampler = "agent";
+  std::string sidecarRing;           // sampler daemon: broadcast name (default: the GPU's BDF)
   uint64_t stepStageSlots = 8192;    // pack_mode step: staged samples between steps (power
                                      // of 2; 8 s at 1 kHz, ~35 MiB pinned for 528 instances)
   int stages = 64;                   // pinned staging batches in flight (<= 256)
@@ -175,6 +185,8 @@ class Agent {
 
  private:
   void samplerLoop();
+  void sidecarLoop();  // sampler "daemon": the daemon's slots -> the staging ring
+  uint32_t phaseAt(uint64_t tsNs) const;  // sidecar thread: the phase active at tsNs
   void controlLoop();
   Json sqttRequest(const Json& req, Json res);
   Json dispatchCountersRequest(const Json& req, Json res);
@@ -223,6 +235,16 @@ class Agent {
   bool stepGatherLocal(hipStream_t stream, uint64_t head, std::string* err);
   uint64_t stepCompleted();          // newest completed launch's end (packMu_)
   std::atomic<uint64_t> stepLaunches_{0}, stagePacked_{0}, stageFull_{0};
+  // sampler "daemon" (the sidecar)
+  bool sidecar_ = false;
+  std::unique_ptr<SlotBroadcastReader> sidecarReader_;
+  std::string sidecarName_;
+  std::atomic<uint64_t> sidecarLost_{0}, sidecarReads_{0};
+  // (CLOCK_MONOTONIC, phase) seen by the sidecar thread each tick: a daemon
+  // slot is tagged with the phase active when it was sampled
+  static constexpr int kPhaseHist = 256;
+  std::pair<uint64_t, uint32_t> phaseHist_[kPhaseHist] = {};
+  int phaseHistN_ = 0;
   std::unique_ptr<Logger> makeLogger();
 
   AgentConfig cfg_;

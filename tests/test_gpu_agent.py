@@ -683,7 +683,7 @@ def test_host_and_device_pack_modes_agree(native_built):
                 a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
             summ = kt.summary(top=50)
             names = [k["name"] for k in summ["top_kernels"]]
-            calls = {k["name"]: k["calls"] for k in summ["top_kernels"]}
+            calls = {k["name"].removesuffix(".kd"): k["calls"] for k in summ["top_kernels"]}
             recs = [r for r in a.memory_records() if "mfma_util" in r and r.get("counter_samples", 0) > 100]
             st = a.stats()
             a.stop()
