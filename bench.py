@@ -231,6 +231,7 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
         # the job-side opt-in alone: a counting context configured, never started
         from dynolog_amd import _native
         env["ROCP_TOOL_LIBRARIES"] = _native.COUNTABLE_LIB
+    child_timeout = getattr(args, "child_timeout_s", 240.0)
     daemon = None
     if daemon_hz > 0:
         countable = True
@@ -251,7 +252,7 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
             # rate): the last answer taken with the job still running
             next_probe = t0 + 3.0
             first = None  # (time, samples) of the first in-job answer: the achieved rate
-            while r.poll() is None and time.time() - t0 < args.child_timeout_s:
+            while r.poll() is None and time.time() - t0 < child_timeout:
                 if time.time() >= next_probe:
                     mon = daemon.rpc({"fn": "getGpuCounterMonitor"}) or {}
                     now = time.time()
@@ -267,11 +268,11 @@ def run_baseline_child(args, tag: str, countable: bool = False, started_once: bo
                     next_probe = time.time() + 2.0
                 time.sleep(0.2)
         try:
-            r.wait(timeout=max(1.0, args.child_timeout_s - (time.time() - t0)))
+            r.wait(timeout=max(1.0, child_timeout - (time.time() - t0)))
         except subprocess.TimeoutExpired:
             r.kill()
             r.wait()
-            raise RuntimeError(f"no-agent child '{tag}' did not finish within {args.child_timeout_s:.0f} s (killed)")
+            raise RuntimeError(f"no-agent child '{tag}' did not finish within {child_timeout:.0f} s (killed)")
         res = {"tag": tag, "rc": r.returncode, "wall_s": round(time.time() - t0, 1), "countable": countable}
         if daemon is not None:
             res["daemon_while_job_ran"] = seen
