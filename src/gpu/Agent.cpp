@@ -241,10 +241,11 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   }
   hostPack_ = cfg_.packMode == "host";
   stepPack_ = cfg_.packMode == "step";
-  if (cfg_.sampler != "agent" && cfg_.sampler != "daemon") {
-    *err = "sampler must be agent or daemon, not '" + cfg_.sampler + "'";
+  if (cfg_.sampler != "agent" && cfg_.sampler != "daemon" && cfg_.sampler != "auto") {
+    *err = "sampler must be agent, daemon or auto, not '" + cfg_.sampler + "'";
     return false;
   }
+  samplerRequested_ = cfg_.sampler;
   sidecar_ = cfg_.sampler == "daemon";
   if (sidecar_ && !stepPack_) {
     *err = "sampler daemon stages the daemon's slots for the step pack kernel: it needs pack_mode step";
@@ -372,6 +373,16 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   passes_.clear();
   sampler_ = nullptr;
   sidecarReader_.reset();
+  if (cfg_.sampler == "auto") {
+    // the daemon's cheaper read when it is there for this GPU: a live
+    // broadcast (heartbeat < 1 s, sampling) of the full counter set; this
+    // process reads the counters itself otherwise
+    std::string e;
+    const std::string name = cfg_.sidecarRing.empty() ? slotBroadcastName(pciLoc_) : cfg_.sidecarRing;
+    auto r = stepPack_ && cfg_.counterPasses.empty() ? SlotBroadcastReader::open(name, &e) : nullptr;
+    sidecar_ = r && r->live(monoNs(), 1'000'000'000ull) && r->header().full_set.load() != 0;
+    cfg_.sampler = sidecar_ ? "daemon" : "agent";
+  }
   if (sidecar_) {
     // the sidecar: the daemon reads the counters; this process only attaches
     // to its slot broadcast for this GPU (named by PCI location: the daemon's
@@ -2469,6 +2480,7 @@ Json Agent::stats() const {
   j["log_intervals_dropped"] = static_cast<unsigned long long>(logDropped_.load());
   j["pack_mode"] = cfg_.packMode;
   j["sampler"] = cfg_.sampler;
+  j["sampler_requested"] = samplerRequested_;
   if (sidecar_) {
     // the daemon reads the counters: its broadcast, and what this agent took
     j["sidecar_ring"] = sidecarName_;

@@ -88,6 +88,8 @@ struct AgentConfig {
   //          agent takes its slots from the daemon's node-local broadcast ring
   //          (SlotBroadcast.h) and tags, packs (pack_mode step), gathers and logs them
   //          exactly as its own -- a sidecar: no counting context runs in the job
+  //   auto   the daemon when a live broadcast of the full counter set exists for this
+  //          GPU (pack_mode step, one counter pass), this process otherwise
   std::string sampler = "agent";
   std::string sidecarRing;           // sampler daemon: broadcast name (default: the GPU's BDF)
   uint64_t stepStageSlots = 8192;    // pack_mode step: staged samples between steps (power
@@ -239,6 +241,7 @@ class Agent {
   bool sidecar_ = false;
   std::unique_ptr<SlotBroadcastReader> sidecarReader_;
   std::string sidecarName_;
+  std::string samplerRequested_;
   std::atomic<uint64_t> sidecarLost_{0}, sidecarReads_{0};
   // (CLOCK_MONOTONIC, phase) seen by the sidecar thread each tick: a daemon
   // slot is tagged with the phase active when it was sampled

@@ -156,6 +156,7 @@ bool DeviceMonitor::start(const Json& cfg, std::string* err) {
       std::string be;
       g->bcast = SlotBroadcastWriter::create(slotBroadcastName(g->pciLoc), broadcastSlots_, g->pciLoc, g->index, hz_, &be);
       if (!g->bcast) LOG(WARNING) << "GPU " << a.index << ": no slot broadcast: " << be;
+      else g->bcast->setFullSet(!g->onAlt);
     }
     gpus_.push_back(std::move(g));
   }
@@ -247,6 +248,7 @@ void DeviceMonitor::switchSet(Gpu* g, size_t cp, uint64_t* prevTs, std::vector<d
   g->onAlt = to;
   g->switches++;
   applyMasks(g);
+  if (g->bcast) g->bcast->setFullSet(!to);
   *prevTs = ok ? (s0 + s1) / 2 : 0;
   std::fill(prev->begin(), prev->end(), 0.0);
   if (!ok) LOG(WARNING) << "GPU " << g->index << " counter set '" << toP.spec.set << "': " << e;

@@ -49,7 +49,8 @@ struct SlotBroadcastHeader {
   double sample_hz;            // the writer's target rate
   std::atomic<uint64_t> heartbeat_ns;  // CLOCK_MONOTONIC of the writer's last tick
   std::atomic<uint32_t> paused;        // 1 while the writer does not sample
-  uint32_t pad0;
+  std::atomic<uint32_t> full_set;      // 1 while it samples the full set (not the readable-only
+                                       // "xproc" set it falls back to beside uncountable jobs)
   uint64_t reserved[24];
 };
 static_assert(sizeof(SlotBroadcastHeader) == 256, "broadcast header is 256 bytes");
@@ -123,6 +124,7 @@ class SlotBroadcastWriter {
     hdr_->heartbeat_ns.store(nowNs, std::memory_order_relaxed);
     hdr_->paused.store(paused ? 1u : 0u, std::memory_order_relaxed);
   }
+  void setFullSet(bool full) { hdr_->full_set.store(full ? 1u : 0u, std::memory_order_relaxed); }
   uint64_t published() const { return hdr_->head.load(std::memory_order_relaxed); }
   const std::string& name() const { return name_; }
 
@@ -196,6 +198,11 @@ class SlotBroadcastReader {
     }
     cursor_ += n;
     return static_cast<size_t>(n - bad);
+  }
+  // a live writer: its heartbeat within maxAgeNs of nowNs, sampling
+  bool live(uint64_t nowNs, uint64_t maxAgeNs) const {
+    const uint64_t hb = hdr_->heartbeat_ns.load(std::memory_order_relaxed);
+    return hb != 0 && nowNs >= hb && nowNs - hb <= maxAgeNs && hdr_->paused.load() == 0;
   }
   // skip everything published so far (e.g. after a pause)
   void skipToHead() { cursor_ = hdr_->head.load(std::memory_order_acquire); }

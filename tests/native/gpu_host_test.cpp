@@ -1061,6 +1061,15 @@ TEST(GpuHost, SlotBroadcastMultiReader) {
   EXPECT_TRUE(WIFEXITED(st) && WEXITSTATUS(st) == 0);
   close(pipefd[0]);
   close(pipefd[1]);
+  // liveness for sampler "auto": a recent heartbeat, sampling, full set
+  EXPECT_FALSE(r1->live(5'000'000'000ull, 1'000'000'000ull));  // no heartbeat yet
+  w->heartbeat(4'500'000'000ull, false);
+  w->setFullSet(true);
+  EXPECT_TRUE(r1->live(5'000'000'000ull, 1'000'000'000ull));
+  EXPECT_EQ(r1->header().full_set.load(), 1u);
+  EXPECT_FALSE(r1->live(6'000'000'000ull, 1'000'000'000ull));  // stale
+  w->heartbeat(5'900'000'000ull, true);
+  EXPECT_FALSE(r1->live(6'000'000'000ull, 1'000'000'000ull));  // paused
   w.reset();  // unlinks
   EXPECT_TRUE(SlotBroadcastReader::open(name, &err) == nullptr);
 }

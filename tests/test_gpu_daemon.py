@@ -481,7 +481,7 @@ def test_agent_sidecar_takes_daemon_slots(native_built):
             x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
             y = x @ x; torch.cuda.synchronize()
             out = {}
-            for sampler in ("daemon", "agent"):
+            for sampler in ("daemon", "agent", "auto"):
                 a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), log_interval_ms=250,
                                          sampler=sampler)
                 t0 = agent.mono_ns()
@@ -522,6 +522,10 @@ def test_agent_sidecar_takes_daemon_slots(native_built):
     assert gemm["samples"] > 100 and idle["samples"] > 100, ph
     assert gemm["mfma_util"] > 10 * max(idle["mfma_util"], 0.1), ph
     assert sc["mfma"] and max(sc["mfma"]) > 5, sc["mfma"]
+    # "auto" takes the daemon's read when its broadcast is live and full
+    au = res["auto"]["st"]
+    assert au["sampler_requested"] == "auto", au
+    assert au["sampler"] == "daemon", (au, mon["gpus"][0])  # an explicit set is always the full one
     g0 = mon["gpus"][0]
     assert g0["late_ticks"] < 0.02 * g0["samples"] + 10, g0
     assert g0["sample_latency_us_avg"] < 500, g0
