@@ -1007,8 +1007,8 @@ void Agent::samplerLoop() {
     bool skipTick = false;
     if (stepPack_) {
       sh = stepHead_.load(std::memory_order_relaxed);
-      if (sh + 2 > stepDone_.load(std::memory_order_acquire) + stepSlots_ &&
-          sh + 2 > stepCompleted() + stepSlots_) {
+      if (!stepStageHasRoom(sh, stepDone_.load(std::memory_order_acquire), stepSlots_) &&
+          !stepStageHasRoom(sh, stepCompleted(), stepSlots_)) {
         stageFull_++;
         skipTick = true;
       }
@@ -1170,7 +1170,8 @@ void Agent::sidecarLoop() {
     if (lost) sidecarLost_ += lost;
     for (size_t i = 0; i < n; ++i) {
       const uint64_t sh = stepHead_.load(std::memory_order_relaxed);
-      if (sh + 2 > stepDone_.load(std::memory_order_acquire) + stepSlots_ && sh + 2 > stepCompleted() + stepSlots_) {
+      if (!stepStageHasRoom(sh, stepDone_.load(std::memory_order_acquire), stepSlots_) &&
+          !stepStageHasRoom(sh, stepCompleted(), stepSlots_)) {
         stageFull_++;  // no step() for a whole staging ring of samples
         continue;
       }

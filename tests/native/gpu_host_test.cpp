@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <string>
 #include <vector>
@@ -1072,4 +1073,55 @@ TEST(GpuHost, SlotBroadcastMultiReader) {
   EXPECT_FALSE(r1->live(6'000'000'000ull, 1'000'000'000ull));  // paused
   w.reset();  // unlinks
   EXPECT_TRUE(SlotBroadcastReader::open(name, &err) == nullptr);
+}
+
+// pack_mode step's staging protocol (stepStageHasRoom, GatherPlan.h) under a
+// random schedule: a sampler stages entries whenever the rule allows, steps
+// launch packs of [tail, head) at random times, launches complete in order
+// after random delays (the GPU may read an entry any time before its launch
+// completes), and the sampler learns completions only through completion
+// marks.  No launch may find any entry it reads -- its range and each
+// sample's predecessor -- overwritten before it completes.
+TEST(GatherPlan, StepStagingNeverOverwritesEntriesALaunchReads) {
+  uint64_t rng = 0x9e3779b97f4a7c15ull;
+  auto rnd = [&](uint64_t n) {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return rng % n;
+  };
+  for (uint64_t slots : {64ull, 256ull}) {
+    std::vector<uint64_t> ring(slots, UINT64_MAX);  // entry index -> sequence it holds
+    struct Launch {
+      uint64_t begin, end, completeAt;
+    };
+    std::deque<Launch> pending;
+    uint64_t head = 0, tail = 0, done = 0, dropped = 0, violations = 0, packed = 0;
+    for (uint64_t t = 0; t < 200000; ++t) {
+      // the sampler: one tick
+      if (stepStageHasRoom(head, done, slots)) {
+        ring[head % slots] = head;
+        ++head;
+      } else {
+        ++dropped;
+      }
+      // a step now and then (sometimes long gaps: the ring fills)
+      if (rnd(t % 5000 < 2500 ? 40 : 900) == 0 && head > tail) {
+        pending.push_back({tail, head, t + 1 + rnd(300)});
+        tail = head;
+      }
+      // launches complete in order; each checks what it read
+      while (!pending.empty() && pending.front().completeAt <= t) {
+        const Launch& l = pending.front();
+        for (uint64_t e = (l.begin ? l.begin - 1 : 0); e < l.end; ++e)
+          if (ring[e % slots] != e) ++violations;
+        packed += l.end - l.begin;
+        done = l.end;  // the completion mark the sampler queries
+        pending.pop_front();
+      }
+    }
+    EXPECT_EQ(violations, 0u);
+    EXPECT_TRUE(dropped > 0);          // the long gaps did fill the ring
+    EXPECT_TRUE(packed > 30000u);      // and the protocol kept packing
+  }
 }
