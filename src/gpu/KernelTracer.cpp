@@ -139,6 +139,7 @@ bool KernelTracer::start(std::string* err) {
     if (active_) return true;
     recs_.clear();
     dropped_ = 0;
+    staleRecords_ = 0;
     rocprofiler_timestamp_t ts = 0;
     const uint64_t m0 = monoNow();
     rocprofiler_get_timestamp(&ts);
@@ -177,6 +178,13 @@ void KernelTracer::onRecords(const KernelRecord* recs, size_t n, uint64_t droppe
   std::lock_guard<std::mutex> g(mu_);
   for (size_t i = 0; i < n; ++i) {
     KernelRecord r = recs[i];
+    // a record of an earlier window delivered late (the runtime hands some
+    // over after that window's flush, profiles/round5/g03: a dispatch 5 s
+    // before the window in the next capture): not this window's
+    if (r.endNs < windowStart_) {
+      staleRecords_++;
+      continue;
+    }
     auto it = agentIndex_.find(r.agent);
     r.agentIndex = it == agentIndex_.end() ? -1 : it->second;
     recs_.push_back(r);
@@ -249,6 +257,7 @@ Json KernelTracer::summary(size_t topN) const {
   j["gpu_busy_ms"] = busy * 1e-6;
   j["gpu_busy_pct"] = window ? 100.0 * static_cast<double>(busy) / static_cast<double>(window) : 0.0;
   j["dropped_records"] = static_cast<unsigned long long>(dropped_);
+  j["stale_records_skipped"] = static_cast<unsigned long long>(staleRecords_);
   Json top = Json::array();
   for (size_t i = 0; i < order.size() && i < topN; ++i) {
     const auto& a = by[order[i].second];

@@ -98,6 +98,7 @@ class KernelTracer {
   std::map<uint64_t, int> agentIndex_;
   std::vector<KernelRecord> recs_;
   uint64_t dropped_ = 0;
+  uint64_t staleRecords_ = 0;  // late records of an earlier window, skipped
   uint64_t windowStart_ = 0, windowEnd_ = 0;
   int64_t clockOffset_ = 0;  // monotonic - rocprofiler timestamp
 };
