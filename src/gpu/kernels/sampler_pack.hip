@@ -18,9 +18,14 @@
 //  * Per-instance deltas are taken BEFORE reducing so that "max over XCD"
 //    counters (GRBM_GUI_ACTIVE / GRBM_COUNT) are max of deltas, as the
 //    rocprofiler derived-metric formulas require (reduce(GRBM_GUI_ACTIVE,max)).
-//  * Raw doubles come from a pinned staging batch copied H2D by the SDMA
-//    engine, so the kernel never touches PCIe and occupies one CU for a few
-//    microseconds per batch on a low-priority stream.
+//  * Raw doubles come from a pinned staging batch copied H2D with
+//    hipMemcpyAsync on a low-priority stream.  That copy is NOT an SDMA
+//    transfer here: the runtime ran it as `__amd_rocclr_copyBuffer` blit
+//    kernels, 3.5 ms of kernel time per 340 ms training step, concurrent with
+//    the trainer's GEMMs (profiles/round4/g04b) -- the reason pack_mode
+//    "device" is no longer the default.  pack_mode "step" (step_pack.hip)
+//    reads the pinned staging memory from the kernel itself, once per step on
+//    the trainer's stream, with no copy at all.
 //  * The slot is assembled in LDS and stored as 16 x 16-byte lanes
 //    (global_store_dwordx4), one 256-B line per sample.
 #include <hip/hip_runtime.h>
