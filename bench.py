@@ -687,22 +687,40 @@ def _main(args, wd) -> int:
 
     ag = None
     sidecar = None  # the node's daemon (sampler daemon, local rank 0)
+    sidecar_fallback = None
     if use_agent and args.sampler == "daemon":
         wd.phase("sidecar daemon start", 120.0)
+        why = ""
         if env.local_rank == 0:
-            from dynolog_amd.utils.daemon import DaemonProcess
-            sidecar = DaemonProcess(["--enable_gpu_counters", f"--gpu_counter_hz={args.sample_hz}",
-                                     f"--gpu_counters={args.counter_set}",
-                                     "--gpu_counter_reporting_interval_s=3600"]).start()
-            deadline = time.time() + 60
-            mon = {}
-            while time.time() < deadline:  # every GPU's thread publishing slots
-                mon = sidecar.rpc({"fn": "getGpuCounterMonitor"}) or {}
-                if mon.get("status") == "ok" and all(g.get("slots_published", 0) > 0 for g in mon.get("gpus", [{}])):
-                    break
-                time.sleep(0.2)
-            else:
-                raise RuntimeError("sidecar daemon publishes no slots: " + json.dumps(mon)[:2000])
+            try:
+                from dynolog_amd.utils.daemon import DaemonProcess
+                sidecar = DaemonProcess(["--enable_gpu_counters", f"--gpu_counter_hz={args.sample_hz}",
+                                         f"--gpu_counters={args.counter_set}",
+                                         "--gpu_counter_reporting_interval_s=3600"]).start()
+                deadline = time.time() + 60
+                mon = {}
+                while time.time() < deadline:  # every GPU's thread publishing slots
+                    mon = sidecar.rpc({"fn": "getGpuCounterMonitor"}) or {}
+                    if mon.get("status") == "ok" and all(g.get("slots_published", 0) > 0 for g in mon.get("gpus", [{}])):
+                        break
+                    time.sleep(0.2)
+                else:
+                    why = "the daemon published no slots within 60 s: " + json.dumps(mon)[:500]
+            except Exception as e:  # noqa: BLE001 - fall back below, never fail the run for it
+                why = f"the daemon did not start: {e}"[:800]
+        # every node's verdict: one failed node and the whole job samples in process
+        whys = [why]
+        if torch.distributed.is_initialized():
+            whys = [None] * env.world
+            torch.distributed.all_gather_object(whys, why)
+        bad = [w for w in whys if w]
+        if bad:
+            sidecar_fallback = bad[0]
+            print(f"bench: sampler daemon unavailable ({bad[0]}); sampling in process", file=sys.stderr, flush=True)
+            if sidecar is not None:
+                sidecar.stop()
+                sidecar = None
+            args.sampler = "agent"
         pdist.barrier()
         wd.phase("init", args.init_timeout_s)
     if use_agent:
@@ -1037,6 +1055,8 @@ def _main(args, wd) -> int:
         if ag is not None:
             # ranks per gather group (= n_gpus on one node; one group per node otherwise)
             out["gather_group_size"] = ag.gather_world
+        if sidecar_fallback:
+            out["sampler_fallback"] = {"requested": "daemon", "reason": sidecar_fallback}
         if ag is not None and ag.config.get("fallback_from"):
             out["gather_fallback"] = {"requested": ag.config["fallback_from"],
                                       "reason": ag.config.get("fallback_reason", "")}
