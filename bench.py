@@ -1081,7 +1081,9 @@ def _main(args, wd) -> int:
                              "sampler_cpu_pct", "consumer_cpu_pct", "pack_mode", "host_rss_mb",
                              "heap_in_use_mb", "sampler", "step_pack_launches", "step_packed",
                              "step_stage_full_ticks", "gather_skipped_busy", "gather_dropped_busy",
-                             "ring_slots", "ring_in_hbm", "sidecar_lost", "sidecar_daemon_hz")
+                             "ring_slots", "ring_in_hbm", "sidecar_lost", "sidecar_daemon_hz",
+                             "step_host_us_avg", "step_host_us_max", "rccl_settle_waits", "rccl_settle_wait_ms",
+                             "gather_run_ahead_waits", "run_ahead_wait_ms", "recv_ingest_waits")
                             if k in agent_stats}
             out["agent"]["host_rss_mb_after_warmup"] = rss_start
         if args.sampler == "daemon" and env.local_rank == 0:

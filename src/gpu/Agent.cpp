@@ -1227,6 +1227,17 @@ bool Agent::step(hipStream_t stream, std::string* err) {
     return false;
   }
   std::lock_guard<std::mutex> g(stepMu_);
+  // host time of the call: what step() costs the trainer's thread
+  struct HostTimer {
+    Agent* a;
+    uint64_t t0 = monoNs();
+    ~HostTimer() {
+      const uint64_t ns = monoNs() - t0;
+      a->stepHostNs_ += ns;
+      a->stepHostCalls_++;
+      if (ns > a->stepHostMaxNs_) a->stepHostMaxNs_ = ns;
+    }
+  } hostTimer{this};
   steps_++;
   if (paused_) return true;  // every rank pauses at the same program point
   // Inside a hipGraph capture the gather would be frozen with this step's
@@ -1534,7 +1545,9 @@ bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err
       // the host is more than `lag` steps ahead of the GPU: wait for that
       // step's gather (the device still has `lag` steps queued)
       runAheadWaits_++;
+      const uint64_t w0 = monoNs();
       HIP_OK(hipEventSynchronize(agreeDone_[e]), "agreement wait");
+      runAheadWaitNs_ += monoNs() - w0;
     }
     lagged = hAgree_[e];
   }
@@ -1869,14 +1882,18 @@ void Agent::setSampleHz(double hz) {
 
 int Agent::ncclSettle(int result, uint64_t timeoutNs) {
   if (result != ncclInProgress || !comm_) return result;
-  const uint64_t deadline = monoNs() + timeoutNs;
+  const uint64_t t0 = monoNs();
+  const uint64_t deadline = t0 + timeoutNs;
   ncclResult_t st = ncclInProgress;
+  settleWaits_++;
   while (true) {
     if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) return ncclInternalError;
-    if (st != ncclInProgress) return st;
-    if (monoNs() > deadline) return ncclInProgress;
-    usleep(200);
+    if (st != ncclInProgress) break;
+    if (monoNs() > deadline) break;
+    usleep(20);
   }
+  settleWaitNs_ += monoNs() - t0;
+  return st;
 }
 
 void Agent::pause() { paused_ = true; }
@@ -2472,6 +2489,13 @@ Json Agent::stats() const {
   j["gather_backlog"] = static_cast<unsigned long long>(backlogNow_.load());
   j["gather_run_ahead_waits"] = static_cast<unsigned long long>(runAheadWaits_.load());
   j["recv_ingest_waits"] = static_cast<unsigned long long>(recvWaits_.load());
+  // host time inside step() (the trainer's thread), and what it waited on
+  const uint64_t sc = stepHostCalls_.load();
+  j["step_host_us_avg"] = sc ? stepHostNs_.load() * 1e-3 / static_cast<double>(sc) : 0.0;
+  j["step_host_us_max"] = stepHostMaxNs_.load() * 1e-3;
+  j["rccl_settle_waits"] = static_cast<unsigned long long>(settleWaits_.load());
+  j["rccl_settle_wait_ms"] = settleWaitNs_.load() * 1e-6;
+  j["run_ahead_wait_ms"] = runAheadWaitNs_.load() * 1e-6;
   j["steps_skipped_in_graph_capture"] = static_cast<unsigned long long>(captureSkips_.load());
   // steps whose gather waited > 3 ms for the consumer: skipped (slots kept) at
   // world 1, or run with the drain dropped on a collective's rank 0

@@ -361,6 +361,8 @@ class Agent {
   uint64_t collectiveGathers_ = 0;  // gathers issued through RCCL (stepMu_)
   uint32_t recvCap_[kRecv] = {};        // payload cap of the gather in each recv buffer
   std::atomic<uint64_t> gatherBytes_{0}, gatherSlots_{0}, drainBytes_{0}, runAheadWaits_{0}, recvWaits_{0};
+  std::atomic<uint64_t> stepHostNs_{0}, stepHostCalls_{0}, stepHostMaxNs_{0}, settleWaits_{0}, settleWaitNs_{0},
+      runAheadWaitNs_{0};
   std::atomic<uint64_t> backlogNow_{0}, capNow_{0};
   std::atomic<uint64_t> captureSkips_{0};  // step() calls inside a hipGraph capture
   bool gatherCollective(hipStream_t stream, uint64_t head, std::string* err);
