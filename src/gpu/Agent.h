@@ -228,6 +228,7 @@ class Agent {
   std::atomic<uint64_t> stepHead_{0}, stepDone_{0};
   uint64_t stepTail_ = 0;            // stepMu_
   uint64_t stepLastTs_ = 0;          // sampler thread: the last staged sample
+  std::vector<double> stepScratch_;  // sampler thread: the read, before its streaming copy
   bool stepHaveLast_ = false;
   DynoStepPass* dStepPasses_ = nullptr;
   bool setupStepPasses(std::string* err);
