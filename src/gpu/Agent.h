@@ -287,8 +287,7 @@ class Agent {
   std::unique_ptr<ipc::Fabric> ctl_;
 
   // device buffers
-  hipStream_t packStream_ = nullptr;
-  hipStream_t drainStream_ = nullptr;
+  hipStream_t packStream_ = nullptr;  // pack_mode device only; every other agent launch rides the trainer's stream
   DynoRingHeader* dHdr_ = nullptr;
   DynoSlot* dRing_ = nullptr;
   // pack_mode host: the ring lives in pinned host memory (hRing_ on the CPU,
@@ -398,6 +397,13 @@ class Agent {
   uint64_t shmEnq_ = 0;            // payloads handed to the mailbox (stepMu_)
   std::atomic<uint64_t> shmFull_{0};  // steps whose payload waited for a full mailbox
   bool drainShm();                 // rank 0 consumer: ingest every published peer block
+  struct ShmPending {
+    int slot;                      // gathered_[slot] fires when the block has landed
+    uint64_t count;                // the lane's pub value once it has
+  };
+  std::deque<ShmPending> shmPending_;  // ranks > 0: written, not yet published (stepMu_)
+  bool shmDefer(hipStream_t stream, std::string* err);
+  void shmPublishCompleted(bool wait, uint64_t upTo = ~0ull);
   std::mutex stepMu_;
 
   // consumer
