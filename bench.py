@@ -890,7 +890,9 @@ def _main(args, wd) -> int:
             # deliver every sample taken inside the window (untimed catch-up gather)
             ag.pack_pending()
             pdist.barrier()
-            ag.step()
+            # full payload on every rank: the collective path's lagged, agreed
+            # size would leave the window's last samples in the backlog
+            ag.step(catch_up=True)
             sync()
             pdist.barrier()
             # each gather group's aggregator (job rank 0; with per-node groups
@@ -1083,7 +1085,8 @@ def _main(args, wd) -> int:
                              "step_stage_full_ticks", "gather_skipped_busy", "gather_dropped_busy",
                              "ring_slots", "ring_in_hbm", "sidecar_lost", "sidecar_daemon_hz",
                              "step_host_us_avg", "step_host_us_max", "rccl_settle_waits", "rccl_settle_wait_ms",
-                             "gather_run_ahead_waits", "run_ahead_wait_ms", "recv_ingest_waits")
+                             "gather_run_ahead_waits", "run_ahead_wait_ms", "recv_ingest_waits", "slots_dropped_busy",
+                             "step_staged", "collective")
                             if k in agent_stats}
             out["agent"]["host_rss_mb_after_warmup"] = rss_start
         if args.sampler == "daemon" and env.local_rank == 0:
@@ -1137,7 +1140,7 @@ def _main(args, wd) -> int:
                     torch.distributed.all_gather_object(wins, (a0, a1))
                 ag.pack_pending()
                 pdist.barrier()
-                ag.step()
+                ag.step(catch_up=True)
                 sync()
                 pdist.barrier()
                 n = 0

@@ -464,6 +464,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   seq_ = 0;  // fresh ring: host-side cursors restart with it
   gatheredHost_ = 0;
   collectiveGathers_ = 0;
+  catchUpGathers_ = 0;
   sizer_.reset(cfg_.gatherCapSlots, GatherSizer::kQuantum, GatherSizer::kDefaultLag);
   static_assert(kAgree > GatherSizer::kDefaultLag, "agreement entries must outlive the lag");
   gatherBytes_ = gatherSlots_ = drainBytes_ = runAheadWaits_ = recvWaits_ = 0;
@@ -561,8 +562,8 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
       }
     }
   }
-  // every rank records a gather event per step (a collective non-root rank
-  // has no receive buffer but orders its agreement copy after the gather)
+  // gathered_: a shm-mailbox peer publishes its block once this fires;
+  // drained_: rank 0's consumer polls it before reading a receive buffer
   for (int i = 0; i < kRecv; ++i) {
     HIP_OK(hipEventCreateWithFlags(&gathered_[i], hipEventDisableTiming), "event");
     // the consumer thread polls this one (the drain copy is ordered after
@@ -609,6 +610,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
       HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&shmDev_), shm_->base(), 0), "mailbox device ptr");
     }
     shmEnq_ = 0;
+    shmPending_.clear();
   }
 
   agg_.reset(cfg_.world, cfg_.gatherCapSlots);
@@ -1243,7 +1245,7 @@ uint64_t Agent::completedPackHead() {
   return std::max(head, gatheredHost_);
 }
 
-bool Agent::step(hipStream_t stream, std::string* err) {
+bool Agent::step(hipStream_t stream, std::string* err, bool catchUp) {
   if (!running_) {
     if (err) *err = "agent not running";
     return false;
@@ -1324,7 +1326,7 @@ bool Agent::step(hipStream_t stream, std::string* err) {
   }
   harvestGatherTimers();
   const int timer = beginGatherTimer(stream);
-  const bool ok = collective_ ? gatherCollective(stream, head, err)
+  const bool ok = collective_ ? gatherCollective(stream, head, err, catchUp)
                   : stepPack_ ? stepGatherLocal(stream, head, err)
                               : gatherLocal(stream, head, err);
   if (timer >= 0) endGatherTimer(timer, stream);
@@ -1560,9 +1562,10 @@ bool Agent::stepGatherLocal(hipStream_t stream, uint64_t head, std::string* err)
 //   gather_prep  = oldest pending slots (<= cap) + header; stores this rank's need
 //   ncclAllReduce(max) of the needs   -> agreement for gather g + lag
 //   ncclGather / ncclAllGather of header + cap slots per rank over xGMI
-//   drain stream: reduced need -> pinned host; rank 0: compaction kernel writes
-//   world headers + only the real slots into pinned host memory
-bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err) {
+//   then, on the same stream: rank 0's compaction kernel writes world headers
+//   + only the real slots into pinned host memory, and the reduced need with
+//   them; other ranks copy just the reduced need (a 1-lane kernel)
+bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err, bool catchUp) {
   const uint64_t g = collectiveGathers_;
   uint64_t lagged = 0;
   if (g >= sizer_.lag()) {
@@ -1577,7 +1580,10 @@ bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err
     }
     lagged = hAgree_[e];
   }
-  const uint32_t cap = sizer_.capFor(g, lagged);
+  // (a catch-up gather sends the full payload on every rank: the backlog a
+  // lagged size left behind goes in one call)
+  const uint32_t cap = catchUp ? sizer_.maxCap() : sizer_.capFor(g, lagged);
+  if (catchUp) catchUpGathers_++;
   const uint64_t need = head - gatheredHost_;
   const auto rg = planGatherRange(head, gatheredHost_, cap, cfg_.ringSlots);
   const size_t block = gatherBlockBytes(cap);
@@ -2538,6 +2544,7 @@ Json Agent::stats() const {
   j["rccl_settle_wait_ms"] = settleWaitNs_.load() * 1e-6;
   j["run_ahead_wait_ms"] = runAheadWaitNs_.load() * 1e-6;
   j["steps_skipped_in_graph_capture"] = static_cast<unsigned long long>(captureSkips_.load());
+  j["catch_up_gathers"] = static_cast<unsigned long long>(catchUpGathers_.load());
   // steps whose gather waited > 3 ms for the consumer: skipped (slots kept) at
   // world 1, or run with the drain dropped on a collective's rank 0
   j["gather_skipped_busy"] = static_cast<unsigned long long>(gatherSkippedBusy_.load());

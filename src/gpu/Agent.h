@@ -141,7 +141,11 @@ class Agent {
 
   bool start(const AgentConfig& cfg, const void* ncclUniqueId, size_t idLen, std::string* err);
   // Enqueue the rank-0 gather on `stream` (nullptr = legacy default stream).
-  bool step(hipStream_t stream, std::string* err);
+  // catchUp: this gather carries the full payload (gather_cap_slots per rank)
+  // instead of the lagged agreed size, so one call delivers the backlog --
+  // a final delivery after a measured window.  Every rank of the group must
+  // pass the same value at the same call.
+  bool step(hipStream_t stream, std::string* err, bool catchUp = false);
   // Block until every enqueued drain has been consumed (rank 0).
   void flush();
   // Ask the sampler thread to pack its partially filled batch now; returns
@@ -351,8 +355,9 @@ class Agent {
   uint64_t gatheredHost_ = 0;   // slots already handed to a gather (stepMu_)
 
   // Collective payload sizing (GatherPlan.h): each gather max-reduces the
-  // ranks' pending counts into dAgree_[kAgree + e]; the drain stream copies it
-  // to hAgree_[e]; gather g + lag is sized from it.
+  // ranks' pending counts into dAgree_[kAgree + e]; the drain kernel (rank 0)
+  // or a 1-lane copy (other ranks) writes it to hAgree_[e] on the trainer's
+  // stream; gather g + lag is sized from it.
   static constexpr int kAgree = 8;
   GatherSizer sizer_;
   uint64_t* dAgree_ = nullptr;     // [kAgree] send, [kAgree] reduced
@@ -365,7 +370,8 @@ class Agent {
       runAheadWaitNs_{0};
   std::atomic<uint64_t> backlogNow_{0}, capNow_{0};
   std::atomic<uint64_t> captureSkips_{0};  // step() calls inside a hipGraph capture
-  bool gatherCollective(hipStream_t stream, uint64_t head, std::string* err);
+  std::atomic<uint64_t> catchUpGathers_{0};  // step(catchUp) gathers sent at the full payload
+  bool gatherCollective(hipStream_t stream, uint64_t head, std::string* err, bool catchUp);
   bool gatherLocal(hipStream_t stream, uint64_t head, std::string* err);
 
   // Gather latency on the trainer's stream (gather_prep through the end of the

@@ -9,8 +9,9 @@
 // over xGMI and, on rank 0, over PCIe.  The size is therefore agreed:
 //
 //   * each gather also max-reduces every rank's NEED (slots pending at that
-//     step) in a 8-byte ncclAllReduce; the result reaches the host on the
-//     drain stream;
+//     step) in a 8-byte ncclAllReduce; the result reaches the host through
+//     the drain kernel (a 1-lane copy on ranks that do not drain), on the
+//     trainer's stream;
 //   * the payload of gather g is sized from the agreed need of gather g - lag
 //     (capForNeed): every rank reads the same reduced value, so every rank
 //     computes the same size without exchanging anything else.  The host

@@ -13,7 +13,8 @@
 // fallen `entries` payloads behind) the payload is dropped and counted.
 // Single producer / single consumer per lane, host-only; the GPU writes a
 // block through a device pointer of the registered segment and the producer
-// publishes from a stream host callback once that write has completed.
+// publishes it from its next step() (or flush / stop) once the event recorded
+// after that write has fired (Agent::shmDefer).
 #pragma once
 
 #include <atomic>

@@ -331,10 +331,18 @@ def test_rccl_gather_path_with_one_rank(native_built, mode, pack):
         t1 = agent.mono_ns()
         a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
         st = a.stats(); wc = a.window_counts(t0, t1)
+        # a burst the lagged agreed size cannot carry (~500 new slots against a
+        # payload sized for a few per step), then one catch-up gather
+        time.sleep(0.5); a.pack_pending(); a.step(); torch.cuda.synchronize()
+        lagged = a.stats()["gather_backlog"]
+        a.pack_pending(); a.step(catch_up=True); torch.cuda.synchronize(); a.flush()
+        st2 = a.stats()
         a.stop()
-        print("RESULT " + json.dumps(dict(stats=st, wc=wc, window_s=(t1 - t0) * 1e-9)))
+        print("RESULT " + json.dumps(dict(stats=st, wc=wc, window_s=(t1 - t0) * 1e-9, lagged=lagged, st2=st2)))
     """)
     st = res["stats"]
+    assert res["lagged"] > 100, res["lagged"]
+    assert res["st2"]["catch_up_gathers"] == 1 and res["st2"]["gather_backlog"] == 0, res["st2"]
     assert st["collective"] is True and st["pack_mode"] == pack, st
     assert st["last_error"] == "" and not st["gather_failed"], st
     assert st["gathers"] >= 40, st
