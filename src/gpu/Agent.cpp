@@ -221,7 +221,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     *err = "an earlier stop() left a GPU agent thread stuck in the runtime; restart the process";
     return false;
   }
-  if (samplerHold_) {
+  if (hold_.held()) {
     // an on-demand capture (SQTT / dispatch counting, Python API) still
     // programs the SQ: a new counting context now could hang both
     *err = "an on-demand capture still holds the counter sampler; finish it before start()";
@@ -677,7 +677,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   // must not be overwritten when the thread comes up
   setSampleHz(cfg_.sampleHz);
   samplerDone_ = consumerDone_ = ctlDone_ = false;
-  parkedGen_ = holdGen_.load();  // no hold is pending (start() refuses while one is held)
+  hold_.resetAcknowledged();  // no hold is pending (start() refuses while one is held)
   samplerThread_ = std::thread([this] {
     if (sidecar_) sidecarLoop();
     else samplerLoop();
@@ -980,7 +980,7 @@ void Agent::samplerLoop() {
   std::string err;
   bool wasPaused = false;
   while (!stopFlag_) {
-    if (paused_ || samplerHold_) {
+    if (paused_ || hold_.held()) {
       if (staged > 0 && !stepPack_) {  // (step packing stages every sample at once)
         if (!flushBatch(staged, &err)) lastError_ = err;
         staged = 0;
@@ -990,8 +990,7 @@ void Agent::samplerLoop() {
         sampler_->stop();
         wasPaused = true;
       }
-      // holdSampler() waits for its generation: the context is stopped now
-      parkedGen_.store(holdGen_.load(), std::memory_order_release);
+      hold_.acknowledgeParked();  // the context is stopped now (holdSampler waits for this)
       usleep(2000);
       next = monoNs();
       continue;
@@ -1171,8 +1170,8 @@ void Agent::sidecarLoop() {
   const uint64_t tick = 1'000'000;  // 1 ms: the daemon's rate is at most 1 kHz per GPU
   uint64_t next = monoNs();
   while (!stopFlag_) {
-    if (paused_ || samplerHold_) {
-      parkedGen_.store(holdGen_.load(), std::memory_order_release);
+    if (paused_ || hold_.held()) {
+      hold_.acknowledgeParked();
       wasPaused = true;
       usleep(2000);
       next = monoNs();
@@ -1942,20 +1941,17 @@ int Agent::ncclSettle(int result, uint64_t timeoutNs) {
 
 void Agent::pause() { paused_ = true; }
 bool Agent::holdSampler() {
-  // A generation per hold: the loop acknowledges the generation it parked
-  // under, so a release followed at once by another hold waits for the loop
-  // to park AGAIN (it may be restarting its context for the gap between them)
-  // instead of returning on the previous hold's stale "parked".
-  const uint64_t gen = holdGen_.fetch_add(1) + 1;
-  if (samplerHold_.exchange(true)) return false;
+  // A generation per hold (HoldGate.h): a release followed at once by another
+  // hold waits for the loop to park AGAIN instead of returning on the
+  // previous hold's stale acknowledgement.
+  const uint64_t gen = hold_.begin();
+  if (gen == 0) return false;
   // A capture programs the same counters: it may start only once the sampler
   // loop has stopped its device-counting context (a read still in flight
   // when another counting context starts can wait forever).  Normally ~1 ms.
   const uint64_t deadline = monoNs() + 2'000'000'000ull;
-  while (running_ && samplerThread_.joinable() && parkedGen_.load(std::memory_order_acquire) < gen &&
-         monoNs() < deadline)
-    usleep(200);
-  if (running_ && samplerThread_.joinable() && parkedGen_.load() < gen)
+  while (running_ && samplerThread_.joinable() && !hold_.parkedFor(gen) && monoNs() < deadline) usleep(200);
+  if (running_ && samplerThread_.joinable() && !hold_.parkedFor(gen))
     LOG(WARNING) << "GPU agent: the sampler did not park within 2 s for an on-demand capture";
   return true;
 }
@@ -2501,7 +2497,7 @@ Json Agent::stats() const {
   // the GPU this rank's HIP device is, and the GPU its counters are read from
   if (pciLoc_) j["hip_bdf"] = pciLocString(pciLoc_);
   if (sampler_) j["sampled_agent_bdf"] = agentBdf(sampler_->agent());
-  j["sampler_held"] = samplerHold_.load();
+  j["sampler_held"] = hold_.held();
   j["rank"] = cfg_.jobRank();
   j["world"] = cfg_.jobWorld > 0 ? cfg_.jobWorld : cfg_.world;
   // the gather group (= the job unless gather_scope "node" split a multi-node job)

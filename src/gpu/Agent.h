@@ -36,6 +36,7 @@
 
 #include "common/Json.h"
 #include "gpu/GatherPlan.h"
+#include "gpu/HoldGate.h"
 #include "gpu/RocprofSampler.h"
 #include "gpu/SlotAggregator.h"
 #include "gpu/SlotBroadcast.h"
@@ -176,8 +177,8 @@ class Agent {
   // SQ itself (SQTT, dispatch counting); step() keeps gathering, so the
   // ranks' collectives stay matched.  False if the sampler was already held.
   bool holdSampler();
-  void releaseSampler() { samplerHold_ = false; }
-  bool samplerHeld() const { return samplerHold_; }
+  void releaseSampler() { hold_.release(); }
+  bool samplerHeld() const { return hold_.held(); }
   // testing: make the consumer stop ingesting drains (as a stuck consumer
   // would); step() must still return promptly
   void testStallConsumer(bool on) { testStallConsumer_ = on; }
@@ -270,10 +271,7 @@ class Agent {
   // Holds only the sampler thread (on-demand captures from the control
   // thread); unlike paused_ it never gates step(), so a rank in a collective
   // gather keeps issuing its gathers while it is being captured.
-  std::atomic<bool> samplerHold_{false};
-  // holdSampler() generations: holdGen_ counts holds, parkedGen_ is the
-  // newest generation the sampler loop parked under (its context stopped)
-  std::atomic<uint64_t> holdGen_{0}, parkedGen_{0};
+  HoldGate hold_;
   uint64_t pciLoc_ = 0;  // this rank's GPU (DynoGatherHeader::pci_loc)
   // The agent's communicator is non-blocking (init can be abandoned at a
   // deadline): wait for a call that returned ncclInProgress to finish.
