@@ -247,6 +247,7 @@ class Agent {
   bool sidecar_ = false;
   std::unique_ptr<SlotBroadcastReader> sidecarReader_;
   std::string sidecarName_;
+  uint64_t sidecarPciLoc_ = 0;  // pci_loc in the broadcast's header
   std::string samplerRequested_;
   std::atomic<uint64_t> sidecarLost_{0}, sidecarReads_{0};
   // (CLOCK_MONOTONIC, phase) seen by the sidecar thread each tick: a daemon
