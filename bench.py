@@ -1093,6 +1093,7 @@ def _main(args, wd) -> int:
                              "ring_slots", "ring_in_hbm", "sidecar_lost", "sidecar_daemon_hz",
                              "step_host_us_avg", "step_host_us_max", "rccl_settle_waits", "rccl_settle_wait_ms",
                              "gather_run_ahead_waits", "run_ahead_wait_ms", "recv_ingest_waits", "slots_dropped_busy",
+                             "catch_up_gathers",
                              "step_staged", "collective")
                             if k in agent_stats}
             out["agent"]["host_rss_mb_after_warmup"] = rss_start

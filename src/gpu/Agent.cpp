@@ -1636,7 +1636,7 @@ bool Agent::gatherCollective(hipStream_t stream, uint64_t head, std::string* err
   collectiveGathers_++;
   gatheredHost_ = rg.first + rg.count;
   backlogNow_ = rg.backlog;
-  capNow_ = cap;
+  if (!catchUp) capNow_ = cap;  // the agreed size (a catch-up gather is full by design)
   gatherBytes_ += block;
   gatherSlots_ += rg.count;
   gathers_++;

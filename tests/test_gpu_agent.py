@@ -650,12 +650,13 @@ def test_rccl_gather_path_as_non_root_member(native_built, mode):
                 y = x @ x
             a.step()
         torch.cuda.synchronize()
-        a.pack_pending(); a.step(); torch.cuda.synchronize()
+        a.pack_pending(); a.step(catch_up=True); torch.cuda.synchronize()
         st = a.stats(); a.stop()
         print("RESULT " + json.dumps(st))
     """)
     st = res
     assert st["collective"] is True and st["last_error"] == "" and not st["gather_failed"], st
+    assert st["catch_up_gathers"] == 1 and st["gather_backlog"] == 0, st
     assert st["gathers"] >= 40 and st["gather_slots"] > 100, st
     assert st["gather_cap_slots_now"] < 4096, st          # the agreement sized the payload
     assert st["gather_latency_samples"] >= 30, st
