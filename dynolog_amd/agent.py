@@ -423,7 +423,7 @@ class GpuAgent:
               gather_scope: str = "node", force_collective_role: str = "",
               comm_init_timeout_ms: int = 60000, pack_mode: str = "step",
               pin_threads: bool = True, step_stage_slots: int = 8192,
-              sampler: str = "agent", sidecar_ring: str = "") -> "GpuAgent":
+              sampler: str = "agent", sidecar_ring: str = "", sidecar_raw: bool = True) -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
@@ -475,7 +475,10 @@ class GpuAgent:
         /dev/shm; this agent takes them from there, tags them with its rank
         and phases, and gathers / logs them as its own; needs pack_mode
         "step").  ``sidecar_ring`` overrides the broadcast's name (default:
-        the GPU's PCI location)."""
+        the GPU's PCI location).  ``sidecar_raw`` (default): when the
+        broadcast carries the daemon's raw samples, stage those and reduce
+        them with this process's step kernel, as for samples it took itself;
+        False copies the daemon's packed slots instead."""
         if not _preinit_done:
             raise AgentError("dynolog_amd.agent.preinit() must be called before HIP init")
         lib = _native.load_gpu_lib()
@@ -510,6 +513,8 @@ class GpuAgent:
                    sampler=sampler)
         if sidecar_ring:
             cfg["sidecar_ring"] = sidecar_ring
+        if not sidecar_raw:
+            cfg["sidecar_raw"] = False
         if counter_passes:
             cfg["counter_passes"] = counter_passes
         if labels is not None:
@@ -556,7 +561,7 @@ class GpuAgent:
                                   counter_passes=counter_passes, gather_scope=gather_scope,
                                   comm_init_timeout_ms=comm_init_timeout_ms, pack_mode=pack_mode,
                                   pin_threads=pin_threads, step_stage_slots=step_stage_slots,
-                                  sampler=sampler, sidecar_ring=sidecar_ring)
+                                  sampler=sampler, sidecar_ring=sidecar_ring, sidecar_raw=sidecar_raw)
                 # report the mode that was asked for; a chained fallback (RCCL,
                 # then the mailbox) keeps every reason, first failure first
                 inner = agent.config.get("fallback_reason")

@@ -93,6 +93,9 @@ struct AgentConfig {
   //          GPU (pack_mode step, one counter pass), this process otherwise
   std::string sampler = "agent";
   std::string sidecarRing;           // sampler daemon: broadcast name (default: the GPU's BDF)
+  bool sidecarRaw = true;            // sampler daemon: stage the daemon's RAW samples (when its
+                                     // broadcast carries them) and reduce them with this
+                                     // process's step kernel; false: copy its packed slots
   uint64_t stepStageSlots = 8192;    // pack_mode step: staged samples between steps (power
                                      // of 2; 8 s at 1 kHz, ~35 MiB pinned for 528 instances)
   int stages = 64;                   // pinned staging batches in flight (<= 256)
@@ -248,6 +251,17 @@ class Agent {
   std::unique_ptr<SlotBroadcastReader> sidecarReader_;
   std::string sidecarName_;
   uint64_t sidecarPciLoc_ = 0;  // pci_loc in the broadcast's header
+  // raw sidecar: the daemon's counter layouts as step-kernel passes
+  bool sidecarRaw_ = false;
+  struct SidecarLayout {
+    int* dPerm = nullptr;
+    int* dSegStart = nullptr;
+    int* dSegLen = nullptr;
+  };
+  std::vector<SidecarLayout> sidecarLayouts_;
+  uint64_t sidecarLastSrc_ = 0;  // broadcast seq of the newest staged raw sample
+  bool sidecarHaveLast_ = false; // ... and it is the staging ring's newest entry
+  void sidecarStageRaw();        // one pass over the new raw samples (sampler thread)
   std::string samplerRequested_;
   std::atomic<uint64_t> sidecarLost_{0}, sidecarReads_{0};
   // (CLOCK_MONOTONIC, phase) seen by the sidecar thread each tick: a daemon

@@ -109,6 +109,7 @@ class DeviceMonitor {
   bool auto_ = false;
   bool broadcast_ = true;
   uint64_t broadcastSlots_ = 65536;
+  uint64_t broadcastRawSlots_ = 4096;  // raw samples in the broadcast (0: slots only)
   std::atomic<bool> sampling_{true};
   std::thread visThread_;
   std::unique_ptr<ProcScanCache> procCache_;  // visibility thread only
