@@ -71,6 +71,9 @@ def parse_args(argv=None):
                         "slots each rank's agent then tags, packs, gathers and logs (the sidecar), or this "
                         "process's own agent.  The daemon falls back to in-process sampling on every rank "
                         "when it cannot publish (sampler_fallback), and so does a --counter-passes plan")
+    p.add_argument("--sidecar-slots", action="store_true",
+                   help="sampler daemon: copy the daemon's packed slots instead of reducing its raw samples "
+                        "with this process's step kernel (the default)")
     p.add_argument("--counter-set", default="lite", help="lite (default) | full | lean | core | comma list")
     p.add_argument("--counter-passes", default="",
                    help="rotate counter configs per pack batch, e.g. lite:3,precision:1 "
@@ -359,7 +362,8 @@ def matrix_entries(spec: str):
     passes), '@hzN' a sample rate, '@bN' a pack batch, '@kb' the per-window
     kernel breakdown, '@step' / '@host' / '@device' the pack mode, '@fc' the 1-rank RCCL
     gather path, '@daemon' the daemon as sampler (the sidecar; entries without it
-    sample in process), '@sN' N settle steps before each paused window."""
+    sample in process; '@dslots' with it copies the daemon's packed slots instead
+    of reducing its raw samples), '@sN' N settle steps before each paused window."""
     out = []
     for item in [x.strip() for x in spec.split(",") if x.strip()]:
         body, *mods = item.split("@")
@@ -377,6 +381,8 @@ def matrix_entries(spec: str):
                 extra += ["--force-collective"]
             elif m == "daemon":
                 extra += ["--sampler", m]
+            elif m == "dslots":
+                extra += ["--sidecar-slots"]
             elif m.startswith("s") and m[1:].isdigit():
                 extra += ["--pause-settle-steps", m[1:]]
             else:
@@ -739,6 +745,7 @@ def _main(args, wd) -> int:
                                    comm_init_timeout_ms=int(args.comm_init_timeout_s * 1000),
                                    fault_inject=fault_for_rank(args.agent_fault_inject, env.rank),
                                    pack_mode=args.pack_mode, sampler=args.sampler,
+                                   sidecar_raw=not args.sidecar_slots,
                                    force_collective=args.force_collective)
 
     if args.child_started_once:
@@ -1094,7 +1101,7 @@ def _main(args, wd) -> int:
                              "step_host_us_avg", "step_host_us_max", "rccl_settle_waits", "rccl_settle_wait_ms",
                              "gather_run_ahead_waits", "run_ahead_wait_ms", "recv_ingest_waits", "slots_dropped_busy",
                              "catch_up_gathers",
-                             "step_staged", "collective")
+                             "step_staged", "collective", "sidecar_raw", "sidecar_layouts")
                             if k in agent_stats}
             out["agent"]["host_rss_mb_after_warmup"] = rss_start
         if args.sampler == "daemon" and env.local_rank == 0:
