@@ -370,9 +370,12 @@ def test_bench_overhead_matrix_helpers():
         "bench_mod2", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    assert bench.matrix_entries("core, lean,core:3/lite:1,lite@hz500@b128@kb") == [
-        ("core", "core", "", []), ("lean", "lean", "", []), ("core:3/lite:1", "lite", "core:3,lite:1", []),
-        ("lite@hz500@b128@kb", "lite", "", ["--sample-hz", "500.0", "--pack-batch", "128", "--kernel-breakdown"])]
+    # entries sample in process unless they name the daemon sidecar
+    ag = ["--sampler", "agent"]
+    assert bench.matrix_entries("core, lean,core:3/lite:1,lite@hz500@b128@kb,lite@daemon@dslots") == [
+        ("core", "core", "", ag), ("lean", "lean", "", ag), ("core:3/lite:1", "lite", "core:3,lite:1", ag),
+        ("lite@hz500@b128@kb", "lite", "", ag + ["--sample-hz", "500.0", "--pack-batch", "128", "--kernel-breakdown"]),
+        ("lite@daemon@dslots", "lite", "", ["--sampler", "daemon", "--sidecar-slots"])]
     with pytest.raises(SystemExit):
         bench.matrix_entries("lite@x1")
     # overhead = 0.1 % + 0.5 % per million instance reads / s
