@@ -2,7 +2,7 @@
 # Round 5 g11: the full GPU suite in one pass, as the driver runs it.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/r5/g11
+O=$R/gpurun_out/r5/${RUN_ID:-g11}
 mkdir -p $O
 cd $R
 timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gputest.log 2>&1
