@@ -198,6 +198,16 @@ def baseline_child_env(environ, seq: int = 0) -> dict:
 _child_seq = [0]  # no-agent children started by this rank (same order on every rank)
 
 
+def proc_cpu_s(pid: int) -> Optional[float]:
+    """utime + stime of a process (all its threads), seconds; None if gone."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, IndexError, ValueError):
+        return None
+
+
 def run_baseline_child(args, tag: str, countable: bool = False, started_once: bool = False,
                        warmup: Optional[int] = None, paused_agent: bool = False,
                        sampling_agent: bool = False, unpinned: bool = False,
@@ -788,6 +798,7 @@ def _main(args, wd) -> int:
 
         last_loss = [0.0]
         sidecar_stats = [None]  # the daemon's per-GPU sampler state at the end (sampler daemon)
+        sidecar_cpu_pct = [None]  # its CPU use over the headline window, % of one core
         import contextlib
         use_phases = ag is not None and args.phases
 
@@ -883,7 +894,14 @@ def _main(args, wd) -> int:
             kernel_breakdown = summarize_kernel_windows({"active": [kt.summary(top=100000)],
                                                          "paused": [kt.summary(top=100000)]}, args.steps)
         else:
+            # the sidecar daemon's CPU time over the headline window (all its
+            # threads, every GPU of the node): what sampling costs outside the job
+            dcpu0 = proc_cpu_s(sidecar.proc.pid) if sidecar is not None and sidecar.proc else None
             meas_s, m0, m1 = timed(args.steps)
+            if dcpu0 is not None:
+                dcpu1 = proc_cpu_s(sidecar.proc.pid)
+                if dcpu1 is not None and meas_s > 0:
+                    sidecar_cpu_pct[0] = round((dcpu1 - dcpu0) / meas_s * 100.0, 2)
         # per-rank time to finish its own steps inside the headline window
         # (stragglers / imbalance show here; the window itself ends at the barrier),
         # and every rank's window on its own CLOCK_MONOTONIC: samples carry their
@@ -1110,6 +1128,7 @@ def _main(args, wd) -> int:
                 # the daemon's per-GPU threads: do they keep the rate for every GPU?
                 out["sidecar_daemon"] = {
                     "sample_hz": mon.get("sample_hz"),
+                    "cpu_pct_of_one_core": sidecar_cpu_pct[0],
                     "gpus": [{k: g.get(k) for k in ("device", "gpu_bdf", "counter_visibility", "sampling", "samples",
                                                      "sample_latency_us_avg", "sample_latency_us_max", "late_ticks",
                                                      "sample_failures_total", "slots_published")}

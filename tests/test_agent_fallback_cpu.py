@@ -378,6 +378,8 @@ def test_bench_overhead_matrix_helpers():
         ("lite@daemon@dslots", "lite", "", ["--sampler", "daemon", "--sidecar-slots"])]
     with pytest.raises(SystemExit):
         bench.matrix_entries("lite@x1")
+    # the sidecar daemon's CPU time (utime + stime of all its threads)
+    assert bench.proc_cpu_s(os.getpid()) > 0 and bench.proc_cpu_s(2 ** 30) is None
     # overhead = 0.1 % + 0.5 % per million instance reads / s
     pts = [(x, 0.1 + 0.5e-6 * x) for x in (272e3, 336e3, 528e3, 784e3)]
     f = bench.fit_overhead(pts)
