@@ -1131,7 +1131,7 @@ def _main(args, wd) -> int:
                     "cpu_pct_of_one_core": sidecar_cpu_pct[0],
                     "gpus": [{k: g.get(k) for k in ("device", "gpu_bdf", "counter_visibility", "sampling", "samples",
                                                      "sample_latency_us_avg", "sample_latency_us_max", "late_ticks",
-                                                     "sample_failures_total", "slots_published")}
+                                                     "sample_failures_total", "slots_published", "cpu_affinity")}
                              for g in mon.get("gpus", [])]}
         if args.host_pmu != "off":
             # one co-sampler per node (local rank 0): every node's summary

@@ -2,6 +2,7 @@
 
 #include <dirent.h>
 #include <dlfcn.h>
+#include <pthread.h>
 #include <hsa/hsa.h>
 #include <time.h>
 
@@ -11,6 +12,7 @@
 #include <cmath>
 #include <cstring>
 
+#include "collectors/gpu/Topology.h"
 #include "common/Logging.h"
 #include "gpu/Agent.h"
 #include "gpu/SlotDerive.h"
@@ -194,6 +196,17 @@ bool DeviceMonitor::start(const Json& cfg, std::string* err) {
   for (auto& g : gpus_) {
     Gpu* p = g.get();
     p->thread = std::thread([this, p] { loop(p); });
+    // each GPU's thread on CPUs local to that GPU's PCIe root: the CP round
+    // trip of every read stays on the socket that owns the device (8 GPUs of
+    // a node sit on two sockets)
+    if (auto cpus = pciLocalCpus(pciLocString(p->pciLoc))) {
+      cpu_set_t set;
+      CPU_ZERO(&set);
+      for (int c : cpus->cpus())
+        if (c < CPU_SETSIZE) CPU_SET(c, &set);
+      if (CPU_COUNT(&set) > 0 && pthread_setaffinity_np(p->thread.native_handle(), sizeof(set), &set) == 0)
+        p->affinity = cpus->toString();
+    }
   }
   LOG(INFO) << "GPU device-counter monitor: " << gpus_.size() << " GPU(s) at " << hz_ << " Hz, "
             << specs.size() << " counter pass(es) ("
@@ -483,6 +496,7 @@ Json DeviceMonitor::config() {
     o["sample_latency_us_avg"] = g->samplesOk ? g->latSumNs * 1e-3 / static_cast<double>(g->samplesOk) : 0.0;
     o["sample_latency_us_max"] = g->latMaxNs * 1e-3;
     o["late_ticks"] = static_cast<unsigned long long>(g->lateTicks);
+    o["cpu_affinity"] = g->affinity;
     o["sample_failures_total"] = static_cast<unsigned long long>(g->failures);
     if (g->bcast) {
       o["slot_broadcast"] = g->bcast->name();

@@ -97,6 +97,7 @@ class DeviceMonitor {
     // the GPU thread's own timing (mu): sample read latency, ticks missed
     uint64_t samplesOk = 0, latSumNs = 0, latMaxNs = 0, lateTicks = 0;
     std::unique_ptr<SlotBroadcastWriter> bcast;  // node-local slot broadcast (or none)
+    std::string affinity = "unpinned";  // the GPU thread's CPUs (NUMA-local to the GPU when known)
   };
   void loop(Gpu* g);
   void visLoop();                 // the visibility thread

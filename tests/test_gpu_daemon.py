@@ -562,6 +562,7 @@ def test_agent_sidecar_takes_daemon_slots(native_built):
     assert au["sampler"] == "daemon", (au, mon["gpus"][0])  # an explicit set is always the full one
     g0 = mon["gpus"][0]
     assert g0["late_ticks"] < 0.02 * g0["samples"] + 10, g0
+    assert isinstance(g0.get("cpu_affinity"), str), g0  # NUMA-local CPUs, or "unpinned" when unknown
     assert g0["sample_latency_us_avg"] < 500, g0
     if not _runner_holds_gpu():
         # every process on the GPU countable: the daemon samples the full lite
