@@ -367,6 +367,8 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     sidecarHaveLast_ = false;
     sidecarPciLoc_ = sidecarReader_->header().pci_loc;  // the GPU the daemon reads for us
     sidecarLost_ = sidecarReads_ = 0;
+    sidecarStale_ = false;
+    sidecarStaleEvents_ = 0;
     phaseHistN_ = 0;
   } else {
     R_ = 0;
@@ -1478,6 +1480,8 @@ Json Agent::stats() const {
     // raw: this process's step kernel reduces the daemon's raw samples;
     // otherwise it copies the daemon's packed slots
     j["sidecar_raw"] = sidecarRaw_;
+    j["sidecar_stale"] = sidecarStale_.load();
+    j["sidecar_stale_events"] = static_cast<unsigned long long>(sidecarStaleEvents_.load());
     j["sidecar_layouts"] = static_cast<unsigned long long>(sidecarLayouts_.size());
     if (sidecarReader_) {
       const auto& h = sidecarReader_->header();

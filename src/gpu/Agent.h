@@ -261,6 +261,8 @@ class Agent {
   std::vector<SidecarLayout> sidecarLayouts_;
   uint64_t sidecarLastSrc_ = 0;  // broadcast seq of the newest staged raw sample
   bool sidecarHaveLast_ = false; // ... and it is the staging ring's newest entry
+  std::atomic<bool> sidecarStale_{false};          // the daemon's heartbeat is > 3 s old
+  std::atomic<uint64_t> sidecarStaleEvents_{0};    // outages seen
   void sidecarStageRaw();        // one pass over the new raw samples (sampler thread)
   std::string samplerRequested_;
   std::atomic<uint64_t> sidecarLost_{0}, sidecarReads_{0};

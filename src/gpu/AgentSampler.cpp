@@ -389,6 +389,18 @@ void Agent::sidecarLoop() {
     phaseHist_[phaseHistN_ % kPhaseHist] = {now, hPhase_ ? __atomic_load_n(hPhase_, __ATOMIC_ACQUIRE) : 0u};
     ++phaseHistN_;
     if (flushReq_.load() != flushAck_.load()) flushAck_ = flushReq_.load();
+    // failure detection: a daemon that stopped publishing (killed, hung)
+    // leaves a stale heartbeat; say so once per outage (stats sidecar_stale)
+    const uint64_t hb = sidecarReader_->header().heartbeat_ns.load(std::memory_order_relaxed);
+    const bool stale = hb == 0 || now < hb ? false : now - hb > 3'000'000'000ull;
+    if (stale && !sidecarStale_.exchange(true)) {
+      sidecarStaleEvents_++;
+      LOG(WARNING) << "GPU agent: the daemon's broadcast " << sidecarName_ << " has not been updated for "
+                   << (now - hb) / 1000000 << " ms (writer pid " << sidecarReader_->header().writer_pid
+                   << "); no counter samples until it resumes";
+    } else if (!stale && hb != 0 && sidecarStale_.exchange(false)) {
+      LOG(INFO) << "GPU agent: the daemon's broadcast " << sidecarName_ << " is live again";
+    }
     if (sidecarRaw_) {
       sidecarStageRaw();
       next += tick;
