@@ -208,6 +208,14 @@ def proc_cpu_s(pid: int) -> Optional[float]:
         return None
 
 
+def proc_cmdline(pid: int) -> str:
+    try:
+        with open(f"/proc/{pid}/cmdline", "rb") as f:
+            return f.read().replace(b"\0", b" ").decode(errors="replace").strip()[:300]
+    except OSError:
+        return "(gone)"
+
+
 def run_baseline_child(args, tag: str, countable: bool = False, started_once: bool = False,
                        warmup: Optional[int] = None, paused_agent: bool = False,
                        sampling_agent: bool = False, unpinned: bool = False,
@@ -1131,8 +1139,14 @@ def _main(args, wd) -> int:
                     "cpu_pct_of_one_core": sidecar_cpu_pct[0],
                     "gpus": [{k: g.get(k) for k in ("device", "gpu_bdf", "counter_visibility", "sampling", "samples",
                                                      "sample_latency_us_avg", "sample_latency_us_max", "late_ticks",
-                                                     "sample_failures_total", "slots_published", "cpu_affinity")}
+                                                     "sample_failures_total", "slots_published", "cpu_affinity",
+                                                     "compute_pids", "uncountable_pids", "foreign_processes")}
                              for g in mon.get("gpus", [])]}
+                # who the daemon could not count (a process without the agent or
+                # the countable opt-in on that GPU): its command line, to act on
+                unc = sorted({p for g in mon.get("gpus", []) for p in (g.get("uncountable_pids") or [])})
+                if unc:
+                    out["sidecar_daemon"]["uncountable"] = {str(p): proc_cmdline(p) for p in unc[:16]}
         if args.host_pmu != "off":
             # one co-sampler per node (local rank 0): every node's summary
             # reaches the result line, keyed by host when there are several

@@ -229,6 +229,12 @@ const std::vector<LocalGpuProcess>& ProcScanCache::all(uint64_t nowNs) {
 }
 
 namespace {
+// A stand-in must hold real memory on the GPU: a process that only brought
+// the runtime up (the torchrun launcher holds 44 KiB on GPU 0 after torch
+// counted the devices, profiles/round5/g21) has launched nothing.  Any kernel
+// launch loads code objects and kernel arguments into VRAM, far above this.
+constexpr uint64_t kMinStandInVramKiB = 512;
+
 // the visibility logic, over how a process's /proc state is obtained
 template <typename LocalFn, typename CountableFn, typename AllFn>
 GpuVisibility visibilityOf(uint64_t gpuId, const std::string& bdf, int selfPid, const std::vector<KfdProcess>& procs,
@@ -258,7 +264,7 @@ GpuVisibility visibilityOf(uint64_t gpuId, const std::string& bdf, int selfPid, 
       selfHere = true;
       continue;
     }
-    if (seen.count(lp.pid) || vr->second == 0) continue;
+    if (seen.count(lp.pid) || vr->second < kMinStandInVramKiB) continue;
     ++standIns;
     v.pids.push_back(lp.pid);
     if (!countableOf(lp.pid)) v.uncountable.push_back(lp.pid);

@@ -474,6 +474,7 @@ Json DeviceMonitor::config() {
       for (int p : g->vis.uncountable) unc.push_back(p);
       o["compute_pids"] = pids;
       o["uncountable_pids"] = unc;
+      o["foreign_processes"] = g->vis.foreign;  // KFD processes of other PID namespaces (cannot be checked)
       o["gpu_bdf"] = pciLocString(g->pciLoc);
     }
     for (const auto& p : g->passes) {

@@ -910,6 +910,7 @@ TEST(GpuHost, VisibilityAcrossPidNamespaces) {
   t.proc(372, kBdfA, 211184, "7f40-7f41 r--s 0 00:01 9 /memfd:dynolog-countable:555 (deleted)\n");
   t.proc(400, kBdfA, 0, "");
   t.proc(380, kBdfA, 0, "", true);  // opened the GPU, holds no memory on it: not a stand-in
+  t.proc(381, kBdfA, 44, "", true);  // the torchrun launcher: runtime up (44 KiB), no kernel: not one either
   auto v = gpuVisibility(555, kBdfA, 400, t.root + "/kfd", t.root + "/proc");
   ASSERT_EQ(v.pids.size(), 1u);
   EXPECT_EQ(v.pids[0], 372);
