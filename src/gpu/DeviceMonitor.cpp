@@ -192,10 +192,16 @@ bool DeviceMonitor::start(const Json& cfg, std::string* err) {
   // already sampled and logged with the right set and masks
   procCache_ = std::make_unique<ProcScanCache>(procRoot_);
   checkVisibility(monoNs());
-  visThread_ = std::thread([this] { visLoop(); });
+  visThread_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "gpuvis");
+    visLoop();
+  });
   for (auto& g : gpus_) {
     Gpu* p = g.get();
-    p->thread = std::thread([this, p] { loop(p); });
+    p->thread = std::thread([this, p] {
+      pthread_setname_np(pthread_self(), ("gpumon" + std::to_string(p->index)).substr(0, 15).c_str());
+      loop(p);
+    });
     // each GPU's thread on CPUs local to that GPU's PCIe root: the CP round
     // trip of every read stays on the socket that owns the device (8 GPUs of
     // a node sit on two sockets)

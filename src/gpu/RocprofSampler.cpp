@@ -1,12 +1,17 @@
 #include "gpu/RocprofSampler.h"
 
+#include <dirent.h>
 #include <rocprofiler-sdk/device_counting_service.h>
+#include <rocprofiler-sdk/internal_threading.h>
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <set>
 
 #include "common/Logging.h"
 #include "common/System.h"
@@ -40,9 +45,54 @@ rocprofiler_tool_configure_result_t* configureTrampolineForDiscovery(uint32_t v,
 }
 
 namespace {
+// Name the threads the runtime libraries create for themselves ("rp-hsa",
+// "rp-rocprof", ...; otherwise they inherit the process name), so a profile
+// of the job's threads tells them from the trainer's own.  The callbacks run
+// on the creating thread around the pthread_create: the new tid is the one
+// that was not in /proc/self/task before.
+std::set<std::string> taskIds() {
+  std::set<std::string> out;
+  if (DIR* d = opendir("/proc/self/task")) {
+    while (dirent* e = readdir(d))
+      if (e->d_name[0] != '.') out.insert(e->d_name);
+    closedir(d);
+  }
+  return out;
+}
+thread_local std::set<std::string> tlsTasksBefore;
+const char* libTag(rocprofiler_runtime_library_t lib) {
+  switch (lib) {
+    case ROCPROFILER_HSA_LIBRARY: return "rp-hsa";
+    case ROCPROFILER_HIP_LIBRARY: return "rp-hip";
+    case ROCPROFILER_MARKER_LIBRARY: return "rp-marker";
+    case ROCPROFILER_RCCL_LIBRARY: return "rp-rccl";
+    default: return "rp-rocprof";
+  }
+}
+void nameRuntimeThreads() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    rocprofiler_at_internal_thread_create(
+        [](rocprofiler_runtime_library_t, void*) { tlsTasksBefore = taskIds(); },
+        [](rocprofiler_runtime_library_t lib, void*) {
+          for (const auto& t : taskIds()) {
+            if (tlsTasksBefore.count(t)) continue;
+            if (FILE* f = fopen(("/proc/self/task/" + t + "/comm").c_str(), "w")) {
+              fputs(libTag(lib), f);
+              fclose(f);
+            }
+          }
+        },
+        ROCPROFILER_LIBRARY | ROCPROFILER_HSA_LIBRARY | ROCPROFILER_HIP_LIBRARY | ROCPROFILER_MARKER_LIBRARY |
+            ROCPROFILER_RCCL_LIBRARY,
+        nullptr);
+  });
+}
+
 rocprofiler_tool_configure_result_t* configureTrampoline(uint32_t, const char*, uint32_t,
                                                          rocprofiler_client_id_t* id) {
   id->name = "dynolog-amd-agent";
+  nameRuntimeThreads();
   static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t),
                                                  &toolInitTrampoline, &toolFiniTrampoline,
                                                  nullptr};

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Per-thread CPU of a process with the agent, over a few idle seconds:
+--mode none (torch only), countable (libdyno_countable.so), preinit (tool registered, agent never started),
+agent (in-process sampling at 1 kHz), daemon (sidecar; starts its own
+daemon).  Prints one JSON line with the busiest threads (name, CPU %,
+current syscall, wchan)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def threads(pid):
+    out = {}
+    for t in os.listdir(f"/proc/{pid}/task"):
+        try:
+            s = open(f"/proc/{pid}/task/{t}/stat").read()
+            comm = s[s.index("(") + 1:s.rindex(")")]
+            f = s[s.rindex(")") + 2:].split()
+            sc = open(f"/proc/{pid}/task/{t}/syscall").read().split()[0]
+            wchan = open(f"/proc/{pid}/task/{t}/wchan").read().strip()
+            out[int(t)] = (comm, (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK"), sc, wchan)
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="agent", choices=["none", "countable", "preinit", "preinit_nodev", "agent", "daemon"])
+    ap.add_argument("--secs", type=float, default=4.0)
+    a = ap.parse_args()
+    d = None
+    if a.mode == "countable":  # libdyno_countable.so: a counting context configured, never started
+        from dynolog_amd import _native
+        os.environ["ROCP_TOOL_LIBRARIES"] = _native.COUNTABLE_LIB
+    elif a.mode == "preinit_nodev":  # the tool registered, no device counting configured
+        from dynolog_amd import agent
+        agent.preinit(agents=[99])
+    elif a.mode != "none":
+        from dynolog_amd import agent
+        agent.preinit()
+    import torch
+    torch.cuda.set_device(0)
+    x = torch.randn(1024, 1024, device="cuda")
+    (x @ x).sum().item()
+    ag = None
+    if a.mode == "daemon":
+        from dynolog_amd.utils.daemon import DaemonProcess
+        d = DaemonProcess(["--enable_gpu_counters", "--gpu_counter_hz=1000", "--gpu_counters=lite"]).start()
+        time.sleep(3.0)
+    if a.mode in ("agent", "daemon"):
+        ag = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), sampler="daemon" if a.mode == "daemon" else "agent")
+    time.sleep(2.0)
+    pid = os.getpid()
+    t0 = time.time()
+    b0 = threads(pid)
+    time.sleep(a.secs)
+    b1 = threads(pid)
+    dt = time.time() - t0
+    rows = sorted(((b1[t][1] - b0[t][1]) / dt * 100, t, b1[t][0], b1[t][2], b1[t][3]) for t in b1 if t in b0)
+    rows.reverse()
+    st = ag.stats() if ag else {}
+    if ag:
+        ag.stop()
+    if d:
+        d.stop()
+    print(json.dumps({"mode": a.mode, "total_pct": round(sum(r[0] for r in rows), 1),
+                      "threads": [{"tid": t, "name": n, "cpu_pct": round(c, 1), "syscall": sc, "wchan": w}
+                                  for c, t, n, sc, w in rows[:6]],
+                      "samples_taken": st.get("samples_taken")}))
+
+
+if __name__ == "__main__":
+    main()
