@@ -93,6 +93,9 @@ struct AgentConfig {
   //          GPU (pack_mode step, one counter pass), this process otherwise
   std::string sampler = "agent";
   std::string sidecarRing;           // sampler daemon: broadcast name (default: the GPU's BDF)
+  bool sidecarFallback = true;       // raw sidecar: when the daemon's heartbeat is > 3 s old,
+                                     // sample the GPU in this process from then on (its
+                                     // counting context is configured: preinit)
   bool sidecarRaw = true;            // sampler daemon: stage the daemon's RAW samples (when its
                                      // broadcast carries them) and reduce them with this
                                      // process's step kernel; false: copy its packed slots
@@ -262,6 +265,19 @@ class Agent {
   uint64_t sidecarLastSrc_ = 0;  // broadcast seq of the newest staged raw sample
   bool sidecarHaveLast_ = false; // ... and it is the staging ring's newest entry
   std::atomic<bool> sidecarStale_{false};          // the daemon's heartbeat is > 3 s old
+  // Fallback to in-process sampling when the daemon dies (raw sidecar with a
+  // counting context for this GPU): the passes are set up at start (counter
+  // configs only, nothing programmed), their layouts and pass-table entries
+  // (after the daemon's layouts) at the fallback; the sampler thread then
+  // continues as samplerLoop with staging pass_idx offset by passIdxBase_.
+  std::vector<PassState> fallbackPasses_;
+  int agentIdx_ = -1;
+  uint32_t passIdxBase_ = 0;
+  int stepPassCount_ = 1;                          // entries of dStepPasses_
+  std::atomic<bool> sidecarFellBack_{false};
+  std::atomic<uint64_t> sidecarFallbackNs_{0};
+  mutable std::mutex passesMu_;                    // passes_ against stats() while it changes
+  bool sidecarFallback();                          // sampler thread
   std::atomic<uint64_t> sidecarStaleEvents_{0};    // outages seen
   void sidecarStageRaw();        // one pass over the new raw samples (sampler thread)
   std::string samplerRequested_;

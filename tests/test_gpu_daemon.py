@@ -586,17 +586,19 @@ while not os.path.exists(sys.argv[1]):
     for _ in range(4):
         y = x @ x
     a.step(); torch.cuda.synchronize(); time.sleep(0.01)
-st = a.stats(); a.stop()
+t1 = agent.mono_ns()
+a.step(); torch.cuda.synchronize(); a.flush()
+st = a.stats(); st["last_2s"] = a.window_counts(t1 - 2_000_000_000, t1)[0]; a.stop()
 print("RESULT " + json.dumps(st), flush=True)
 """
 
 
 def test_sidecar_reports_a_dead_daemon(native_built):
-    """Failure detection on the sidecar: the daemon is killed (SIGKILL, its
-    broadcast segment left behind with a frozen heartbeat) while a job's agent
-    reads it.  The job keeps training; the agent flags the outage
-    (sidecar_stale, one event, a warning) instead of silently reporting a
-    zero rate."""
+    """Failure detection and recovery on the sidecar: the daemon is killed
+    (SIGKILL, its broadcast segment left behind with a frozen heartbeat) while
+    a job's agent reads it.  The job keeps training; the agent flags the
+    outage (sidecar_stale, one event, a warning) and takes the GPU's sampling
+    over in process: its own samples keep arriving at ~1 kHz."""
     flag = os.path.join(tempfile.mkdtemp(prefix="dyside"), "done")
     d = DaemonProcess(["--enable_gpu_counters", "--gpu_counter_hz=1000", "--gpu_counters=lite"]).start()
     try:
@@ -611,7 +613,7 @@ def test_sidecar_reports_a_dead_daemon(native_built):
             time.sleep(1.0)
             d.proc.kill()  # no clean shutdown: the segment stays, its heartbeat stops
             d.proc.wait(timeout=30)
-            time.sleep(5.0)
+            time.sleep(7.0)  # 3 s to call it stale, then in-process sampling
             rc = c.finish(flag, timeout=60)
             res = [json.loads(l[7:]) for l in c.lines("RESULT ")]
             assert rc == 0 and res, c.tails()
@@ -619,6 +621,9 @@ def test_sidecar_reports_a_dead_daemon(native_built):
             assert st["sampler"] == "daemon" and st["samples_taken"] > 500, st
             assert st["sidecar_stale"] is True and st["sidecar_stale_events"] == 1, st
             assert "has not been updated" in c.stderr(), c.tails()
+            assert st["sidecar_fell_back"] is True and st["sidecar_fallback_after_ms"] > 0, st
+            assert st["last_2s"] > 1500, st  # the job's own 1 kHz after the fallback
+            assert st["samples_failed"] == 0 and st["last_error"] == "", st
     finally:
         d.stop()
         # the killed writer could not unlink its segment
