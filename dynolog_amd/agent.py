@@ -423,7 +423,8 @@ class GpuAgent:
               gather_scope: str = "node", force_collective_role: str = "",
               comm_init_timeout_ms: int = 60000, pack_mode: str = "step",
               pin_threads: bool = True, step_stage_slots: int = 8192,
-              sampler: str = "agent", sidecar_ring: str = "", sidecar_raw: bool = True) -> "GpuAgent":
+              sampler: str = "agent", sidecar_ring: str = "", sidecar_raw: bool = True,
+              sidecar_fallback: bool = True) -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
@@ -478,7 +479,10 @@ class GpuAgent:
         the GPU's PCI location).  ``sidecar_raw`` (default): when the
         broadcast carries the daemon's raw samples, stage those and reduce
         them with this process's step kernel, as for samples it took itself;
-        False copies the daemon's packed slots instead."""
+        False copies the daemon's packed slots instead.  ``sidecar_fallback``
+        (default): if the daemon stops publishing for 3 s, this process takes
+        its GPU's sampling over (its counting context is configured by
+        preinit), and carries on as an in-process agent."""
         if not _preinit_done:
             raise AgentError("dynolog_amd.agent.preinit() must be called before HIP init")
         lib = _native.load_gpu_lib()
@@ -515,6 +519,8 @@ class GpuAgent:
             cfg["sidecar_ring"] = sidecar_ring
         if not sidecar_raw:
             cfg["sidecar_raw"] = False
+        if not sidecar_fallback:
+            cfg["sidecar_fallback"] = False
         if counter_passes:
             cfg["counter_passes"] = counter_passes
         if labels is not None:
@@ -561,7 +567,8 @@ class GpuAgent:
                                   counter_passes=counter_passes, gather_scope=gather_scope,
                                   comm_init_timeout_ms=comm_init_timeout_ms, pack_mode=pack_mode,
                                   pin_threads=pin_threads, step_stage_slots=step_stage_slots,
-                                  sampler=sampler, sidecar_ring=sidecar_ring, sidecar_raw=sidecar_raw)
+                                  sampler=sampler, sidecar_ring=sidecar_ring, sidecar_raw=sidecar_raw,
+                                  sidecar_fallback=sidecar_fallback)
                 # report the mode that was asked for; a chained fallback (RCCL,
                 # then the mailbox) keeps every reason, first failure first
                 inner = agent.config.get("fallback_reason")

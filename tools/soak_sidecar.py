@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""Soak of the always-on sidecar: a node daemon samples the GPU at 1 kHz and
+broadcasts raw samples; a training-like loop's agent (sampler "daemon")
+stages them, reduces them with its step kernel and gathers them every step.
+Every --every seconds it records the delivered rate, entries lost, the
+staging ring, and both processes' resident memory (the job's RSS / heap, the
+daemon's RSS from /proc), printing one line per round; the summary fits the
+memory growth over the second half.
+
+    python tools/soak_sidecar.py --minutes 6 --out gpurun_out/soak_sidecar.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def rss_mb(pid="self") -> float:
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for line in f:
+                if line.startswith("VmRSS:"):
+                    return int(line.split()[1]) / 1024.0
+    except OSError:
+        pass
+    return 0.0
+
+
+def slope(xs, ys):
+    n = len(xs)
+    if n < 2:
+        return 0.0
+    mx, my = sum(xs) / n, sum(ys) / n
+    den = sum((x - mx) ** 2 for x in xs)
+    return sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / den if den else 0.0
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--minutes", type=float, default=6.0)
+    ap.add_argument("--every", type=float, default=30.0)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    from dynolog_amd import agent
+    agent.preinit()
+    import torch
+    from dynolog_amd.utils.daemon import DaemonProcess
+    torch.cuda.set_device(0)
+    x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    (x @ x).sum().item()
+    rounds = []
+    with DaemonProcess(["--enable_gpu_counters", "--gpu_counter_hz=1000", "--gpu_counters=lite",
+                        "--gpu_counter_reporting_interval_s=60"]) as d:
+        t_wait = time.time() + 60
+        while time.time() < t_wait:
+            mon = d.rpc({"fn": "getGpuCounterMonitor"})
+            if mon.get("status") == "ok" and mon["gpus"][0].get("slots_published", 0) > 100:
+                break
+            time.sleep(0.2)
+        ag = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), log_interval_ms=1000, sampler="daemon")
+        t0 = time.time()
+        end = t0 + a.minutes * 60
+        next_round = t0 + a.every
+        last = (agent.mono_ns(), 0)
+        while time.time() < end:
+            for _ in range(8):
+                y = x @ x
+            y = y * 0.5 + x
+            ag.step()
+            torch.cuda.synchronize()
+            if time.time() >= next_round:
+                next_round += a.every
+                ag.step(catch_up=True)
+                torch.cuda.synchronize()
+                ag.flush()
+                now = agent.mono_ns()
+                st = ag.stats()
+                mon = d.rpc({"fn": "getGpuCounterMonitor"})
+                g0 = (mon.get("gpus") or [{}])[0]
+                delivered = ag.window_counts(last[0], now)[0]
+                r = {"t_s": round(time.time() - t0, 1), "delivered_per_s": round(delivered / ((now - last[0]) * 1e-9), 1),
+                     "samples_taken": st.get("samples_taken"), "sidecar_lost": st.get("sidecar_lost"),
+                     "step_stage_full_ticks": st.get("step_stage_full_ticks"), "sidecar_stale": st.get("sidecar_stale"),
+                     "job_rss_mb": round(rss_mb(), 1), "job_heap_mb": round(st.get("heap_in_use_mb", 0.0), 1),
+                     "daemon_rss_mb": round(rss_mb(d.proc.pid), 1), "daemon_late_ticks": g0.get("late_ticks"),
+                     "daemon_latency_us": round(g0.get("sample_latency_us_avg", 0.0), 1)}
+                rounds.append(r)
+                last = (now, 0)
+                print(json.dumps(r), flush=True)
+        ag.stop()
+    half = [r for r in rounds if r["t_s"] >= a.minutes * 30]
+    ts = [r["t_s"] for r in half]
+    summary = {"minutes": a.minutes, "rounds": len(rounds),
+               "delivered_per_s_min": min((r["delivered_per_s"] for r in rounds), default=None),
+               "delivered_per_s_mean": round(sum(r["delivered_per_s"] for r in rounds) / max(len(rounds), 1), 1),
+               "sidecar_lost_end": rounds[-1]["sidecar_lost"] if rounds else None,
+               "job_rss_mb_per_min_2nd_half": round(slope(ts, [r["job_rss_mb"] for r in half]) * 60, 3),
+               "job_heap_mb_per_min_2nd_half": round(slope(ts, [r["job_heap_mb"] for r in half]) * 60, 3),
+               "daemon_rss_mb_per_min_2nd_half": round(slope(ts, [r["daemon_rss_mb"] for r in half]) * 60, 3),
+               "daemon_late_ticks_end": rounds[-1]["daemon_late_ticks"] if rounds else None}
+    print(json.dumps({"summary": summary}), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"summary": summary, "rounds": rounds}, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
