@@ -800,11 +800,23 @@ def _main(args, wd) -> int:
             else:
                 ag.pause()
             if sidecar is not None:  # the daemon's reads are the sampling then
-                sidecar.rpc({"fn": "setGpuCounterMonitor", "enable": on})
+                sidecar_rpc({"fn": "setGpuCounterMonitor", "enable": on})
             if hpmu is not None:
                 hpmu.set_enabled(on)
 
         last_loss = [0.0]
+        sidecar_errors = []
+
+        def sidecar_rpc(req):
+            """A daemon that died mid-run must not end the run: the agents take
+            the sampling over (sidecar fallback); the error is reported."""
+            try:
+                return sidecar.rpc(req)
+            except Exception as e:  # noqa: BLE001
+                if not sidecar_errors:
+                    print(f"bench: sidecar daemon RPC failed ({e}); continuing", file=sys.stderr, flush=True)
+                sidecar_errors.append(str(e)[:200])
+                return None
         sidecar_stats = [None]  # the daemon's per-GPU sampler state at the end (sampler daemon)
         sidecar_cpu_pct = [None]  # its CPU use over the headline window, % of one core
         import contextlib
@@ -1010,7 +1022,7 @@ def _main(args, wd) -> int:
             pdist.barrier()
             ag.pause()
             if sidecar is not None:
-                sidecar_stats[0] = sidecar.rpc({"fn": "getGpuCounterMonitor"})
+                sidecar_stats[0] = sidecar_rpc({"fn": "getGpuCounterMonitor"})
                 sidecar.stop()  # no daemon while the no-agent children run
                 sidecar = None
             if hpmu is not None:
@@ -1099,6 +1111,8 @@ def _main(args, wd) -> int:
             out["gather_group_size"] = ag.gather_world
         if sidecar_fallback:
             out["sampler_fallback"] = {"requested": "daemon", "reason": sidecar_fallback}
+        if sidecar_errors:
+            out["sidecar_rpc_errors"] = {"count": len(sidecar_errors), "first": sidecar_errors[0]}
         if ag is not None and ag.config.get("fallback_from"):
             out["gather_fallback"] = {"requested": ag.config["fallback_from"],
                                       "reason": ag.config.get("fallback_reason", "")}
@@ -1131,7 +1145,7 @@ def _main(args, wd) -> int:
                             if k in agent_stats}
             out["agent"]["host_rss_mb_after_warmup"] = rss_start
         if args.sampler == "daemon" and env.local_rank == 0:
-            mon = sidecar_stats[0] or (sidecar.rpc({"fn": "getGpuCounterMonitor"}) if sidecar is not None else None)
+            mon = sidecar_stats[0] or (sidecar_rpc({"fn": "getGpuCounterMonitor"}) if sidecar is not None else None)
             if mon and mon.get("status") == "ok":
                 # the daemon's per-GPU threads: do they keep the rate for every GPU?
                 out["sidecar_daemon"] = {
