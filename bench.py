@@ -171,7 +171,8 @@ def parse_args(argv=None):
                    help="fixed allowance of each warm-up / timed-window / settle deadline")
     p.add_argument("--child-timeout-s", type=float, default=240.0,
                    help="deadline of one no-agent baseline child")
-    p.add_argument("--fault-hang", default="", help=argparse.SUPPRESS)  # RANK@STEP: that rank hangs there
+    p.add_argument("--fault-hang", default="", help=argparse.SUPPRESS)
+    p.add_argument("--fault-kill-daemon", type=int, default=0, help=argparse.SUPPRESS)  # STEP: the sidecar daemon dies  # RANK@STEP: that rank hangs there
     p.add_argument("--force-collective", action="store_true",
                    help="world 1: gather through a 1-rank RCCL communicator (prices the collective path's "
                         "per-step gather on a one-GPU box)")
@@ -836,6 +837,11 @@ def _main(args, wd) -> int:
                 wd.progress(n, "start")
                 while True:  # fault injection: this rank stops in its own work
                     time.sleep(1.0)
+            if args.fault_kill_daemon and n == args.fault_kill_daemon and sidecar is not None and sidecar.proc:
+                # fault injection: the node's sidecar daemon dies (SIGKILL, its own pid)
+                print(f"bench: fault injection: killing the sidecar daemon (pid {sidecar.proc.pid}) at step {n}",
+                      file=sys.stderr, flush=True)
+                sidecar.proc.kill()
             with ph("forward"):
                 wd.progress(n, "forward")
                 logits = model(inputs)
@@ -1141,7 +1147,8 @@ def _main(args, wd) -> int:
                              "step_host_us_avg", "step_host_us_max", "rccl_settle_waits", "rccl_settle_wait_ms",
                              "gather_run_ahead_waits", "run_ahead_wait_ms", "recv_ingest_waits", "slots_dropped_busy",
                              "catch_up_gathers",
-                             "step_staged", "collective", "sidecar_raw", "sidecar_layouts")
+                             "step_staged", "collective", "sidecar_raw", "sidecar_layouts", "sidecar_stale",
+                             "sidecar_fell_back", "sidecar_fallback_after_ms")
                             if k in agent_stats}
             out["agent"]["host_rss_mb_after_warmup"] = rss_start
         if args.sampler == "daemon" and env.local_rank == 0:
