@@ -147,7 +147,7 @@ std::unique_ptr<Logger> Agent::makeLogger() {
   return std::make_unique<CompositeLogger>(std::move(ls));
 }
 
-bool Agent::setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::string* err) {
+bool Agent::setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::string* err, hipStream_t copy) {
   std::vector<int> counterOf;
   if (!ps.sampler->buildLayout(ids.data(), ids.size(), &counterOf, err)) return false;
   const int C = DC_NUM_COUNTERS;
@@ -168,6 +168,13 @@ bool Agent::setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::st
   HIP_OK(hipMalloc(&ps.dPerm, std::max<size_t>(perm.size(), 1) * sizeof(int)), "hipMalloc perm");
   HIP_OK(hipMalloc(&ps.dSegStart, C * sizeof(int)), "hipMalloc seg");
   HIP_OK(hipMalloc(&ps.dSegLen, C * sizeof(int)), "hipMalloc seg");
+  if (copy) {
+    HIP_OK(hipMemcpyAsync(ps.dPerm, perm.data(), perm.size() * sizeof(int), hipMemcpyHostToDevice, copy), "cp");
+    HIP_OK(hipMemcpyAsync(ps.dSegStart, segStart.data(), C * sizeof(int), hipMemcpyHostToDevice, copy), "cp");
+    HIP_OK(hipMemcpyAsync(ps.dSegLen, segLen.data(), C * sizeof(int), hipMemcpyHostToDevice, copy), "cp");
+    HIP_OK(hipStreamSynchronize(copy), "cp sync");  // the host vectors die here
+    return true;
+  }
   HIP_OK(hipMemcpy(ps.dPerm, perm.data(), perm.size() * sizeof(int), hipMemcpyHostToDevice), "cp");
   HIP_OK(hipMemcpy(ps.dSegStart, segStart.data(), C * sizeof(int), hipMemcpyHostToDevice), "cp");
   HIP_OK(hipMemcpy(ps.dSegLen, segLen.data(), C * sizeof(int), hipMemcpyHostToDevice), "cp");

@@ -219,7 +219,10 @@ class Agent {
     std::vector<int> counterOf;  // record index -> counter slot (host pack)
     uint32_t counterMask = 0;    // delta[] positions this set selects (every slot carries it)
   };
-  bool setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::string* err);
+  // copy: nullptr = synchronous copies on the null stream (at start); a
+  // non-blocking stream keeps a mid-run setup (the sidecar fallback) from
+  // waiting behind the trainer's queued work on the null stream
+  bool setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::string* err, hipStream_t copy = nullptr);
   void switchPass();  // sampler thread: stop the current pass, start the next
   void releaseDevice();
   void waitSamplesThrough(uint64_t t1) const;  // rank 0: samples up to t1 ingested (<= 1 s)

@@ -529,6 +529,14 @@ bool Agent::sidecarFallback() {
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
   const uint32_t base = static_cast<uint32_t>(sidecarLayouts_.size());
   std::vector<DynoStepPass> t(fallbackPasses_.size());
+  // uploads on a private non-blocking stream: the null stream would queue
+  // them behind the trainer's work (seconds of run-ahead, profiles/round5/g30)
+  hipStream_t copy = nullptr;
+  HIP_OK(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking), "fallback stream");
+  struct StreamGuard {
+    hipStream_t s;
+    ~StreamGuard() { (void)hipStreamDestroy(s); }
+  } guard{copy};
   for (size_t i = fallbackPasses_.size(); i-- > 0;) {
     PassState& ps = fallbackPasses_[i];
     ps.sampler->select();
@@ -536,7 +544,7 @@ bool Agent::sidecarFallback() {
     std::vector<double> vals(ps.R);
     std::vector<uint64_t> ids(ps.R);
     size_t n = ps.R;
-    ok = ok && ps.sampler->sample(vals.data(), &n, ids.data(), err) && n == ps.R && setupLayout(ps, ids, err);
+    ok = ok && ps.sampler->sample(vals.data(), &n, ids.data(), err) && n == ps.R && setupLayout(ps, ids, err, copy);
     if (!ok) {
       ps.sampler->stop();
       LOG(ERROR) << "GPU agent: in-process fallback failed (" << e << "); waiting for the daemon";
@@ -553,8 +561,9 @@ bool Agent::sidecarFallback() {
     t[i].pass = ps.spec.pass;
     t[i].counter_mask = ps.counterMask;
   }
-  HIP_OK(hipMemcpy(dStepPasses_ + base, t.data(), t.size() * sizeof(DynoStepPass), hipMemcpyHostToDevice),
+  HIP_OK(hipMemcpyAsync(dStepPasses_ + base, t.data(), t.size() * sizeof(DynoStepPass), hipMemcpyHostToDevice, copy),
          "fallback pass table");
+  HIP_OK(hipStreamSynchronize(copy), "fallback pass table sync");
   {
     std::lock_guard<std::mutex> g(passesMu_);
     passes_ = std::move(fallbackPasses_);
