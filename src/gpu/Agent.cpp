@@ -1523,7 +1523,10 @@ Json Agent::stats() const {
     // otherwise it copies the daemon's packed slots
     j["sidecar_raw"] = sidecarRaw_;
     j["sidecar_stale"] = sidecarStale_.load();
-    j["sidecar_fallback_armed"] = !fallbackPasses_.empty() || sidecarFellBack_.load();
+    {
+      std::lock_guard<std::mutex> g(passesMu_);  // the fallback moves these on the sampler thread
+      j["sidecar_fallback_armed"] = !fallbackPasses_.empty() || sidecarFellBack_.load();
+    }
     j["sidecar_fell_back"] = sidecarFellBack_.load();
     if (sidecarFellBack_.load())
       j["sidecar_fallback_after_ms"] = (sidecarFallbackNs_.load() - startNs_) * 1e-6;

@@ -548,6 +548,7 @@ bool Agent::sidecarFallback() {
     if (!ok) {
       ps.sampler->stop();
       LOG(ERROR) << "GPU agent: in-process fallback failed (" << e << "); waiting for the daemon";
+      std::lock_guard<std::mutex> g(passesMu_);
       fallbackPasses_.clear();
       return false;
     }
