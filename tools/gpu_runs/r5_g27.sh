@@ -2,7 +2,7 @@
 # Round 5 g27: agent, kernel and daemon tests after the sidecar fallback.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/r5/g27
+O=$R/gpurun_out/r5/${RUN_ID:-g27}
 mkdir -p $O
 cd $R
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
