@@ -737,7 +737,10 @@ def _main(args, wd) -> int:
                         break
                     time.sleep(0.2)
                 else:
-                    why = "the daemon published no slots within 60 s: " + json.dumps(mon)[:500]
+                    # some GPUs publish: their ranks take the daemon's read, the
+                    # others sample in process (each agent decides: sampler "auto")
+                    if not any(g.get("slots_published", 0) > 0 for g in mon.get("gpus", [])):
+                        why = "the daemon published no slots within 60 s: " + json.dumps(mon)[:500]
             except Exception as e:  # noqa: BLE001 - fall back below, never fail the run for it
                 why = f"the daemon did not start: {e}"[:800]
         # every node's verdict: one failed node and the whole job samples in process
@@ -763,7 +766,11 @@ def _main(args, wd) -> int:
                                    sinks=("json", "memory"),
                                    comm_init_timeout_ms=int(args.comm_init_timeout_s * 1000),
                                    fault_inject=fault_for_rank(args.agent_fault_inject, env.rank),
-                                   pack_mode=args.pack_mode, sampler=args.sampler,
+                                   pack_mode=args.pack_mode,
+                                   # with a node daemon up, each rank takes its GPU's broadcast when
+                                   # that is live, else samples in process (a GPU the daemon could
+                                   # not start on costs only that rank the cheaper read)
+                                   sampler="auto" if args.sampler == "daemon" else args.sampler,
                                    sidecar_raw=not args.sidecar_slots,
                                    force_collective=args.force_collective)
 
@@ -1127,6 +1134,7 @@ def _main(args, wd) -> int:
             # and its gather cost on the trainer's stream
             st = ag.stats()
             mine = {"rank": env.rank, "hip_bdf": st.get("hip_bdf"), "sampled_agent_bdf": st.get("sampled_agent_bdf"),
+                    "sampler": st.get("sampler"),
                     "gather_latency_us_avg": round(st.get("gather_latency_us_avg", 0.0), 2),
                     "gathers": st.get("gathers")}
             ranks = [None] * env.world
