@@ -3,7 +3,7 @@
 # rehearsals and the headline.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/r5/g28
+O=$R/gpurun_out/r5/${RUN_ID:-g28}
 mkdir -p $O
 cd $R
 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_multirank_gpu.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
