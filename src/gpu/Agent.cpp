@@ -349,6 +349,8 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   passIdxBase_ = 0;
   sidecarFellBack_ = false;
   sidecarFallbackNs_ = 0;
+  sidecarFallbackCause_ = 0;
+  sidecarReducedSinceNs_ = 0;
   sampler_ = nullptr;
   sidecarReader_.reset();
   if (cfg_.sampler == "auto") {
@@ -1528,8 +1530,10 @@ Json Agent::stats() const {
       j["sidecar_fallback_armed"] = !fallbackPasses_.empty() || sidecarFellBack_.load();
     }
     j["sidecar_fell_back"] = sidecarFellBack_.load();
-    if (sidecarFellBack_.load())
+    if (sidecarFellBack_.load()) {
       j["sidecar_fallback_after_ms"] = (sidecarFallbackNs_.load() - startNs_) * 1e-6;
+      j["sidecar_fallback_cause"] = sidecarFallbackCause_.load() == 2 ? "reduced_set" : "daemon_stale";
+    }
     j["sidecar_stale_events"] = static_cast<unsigned long long>(sidecarStaleEvents_.load());
     j["sidecar_layouts"] = static_cast<unsigned long long>(sidecarLayouts_.size());
     if (sidecarReader_) {

@@ -280,7 +280,11 @@ class Agent {
   std::atomic<bool> sidecarFellBack_{false};
   std::atomic<uint64_t> sidecarFallbackNs_{0};
   mutable std::mutex passesMu_;                    // passes_ against stats() while it changes
-  bool sidecarFallback();                          // sampler thread
+  bool sidecarFallback(const char* why);           // sampler thread
+  // why it fell back: 1 the daemon stopped publishing, 2 it dropped to its
+  // readable-only set (an uncountable process joined the GPU)
+  std::atomic<int> sidecarFallbackCause_{0};
+  uint64_t sidecarReducedSinceNs_ = 0;             // sampler thread
   std::atomic<uint64_t> sidecarStaleEvents_{0};    // outages seen
   void sidecarStageRaw();        // one pass over the new raw samples (sampler thread)
   std::string samplerRequested_;

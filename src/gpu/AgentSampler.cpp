@@ -399,9 +399,28 @@ void Agent::sidecarLoop() {
                    << (fallbackPasses_.empty() ? "; no counter samples until it resumes"
                                                : "; sampling the GPU in this process from now on");
       // take the GPU's sampling over: the thread continues as samplerLoop
-      if (!fallbackPasses_.empty() && sidecarFallback()) return;
+      sidecarFallbackCause_ = 1;
+      if (!fallbackPasses_.empty() && sidecarFallback("the daemon stopped publishing")) return;
+      sidecarFallbackCause_ = 0;
     } else if (!stale && hb != 0 && sidecarStale_.exchange(false)) {
       LOG(INFO) << "GPU agent: the daemon's broadcast " << sidecarName_ << " is live again";
+    }
+    // A daemon on --gpu_counters=auto drops to its readable-only set while an
+    // uncountable process shares the GPU. This process can still read its own
+    // waves' counters, so after 1 s on the reduced set it samples in process,
+    // as sampler "auto" would have chosen at start. The daemon's context and
+    // this one read side by side without disturbing either's values
+    // (profiles/round5/g38).
+    if (!stale && !fallbackPasses_.empty()) {
+      if (sidecarReader_->header().full_set.load(std::memory_order_relaxed) != 0) {
+        sidecarReducedSinceNs_ = 0;
+      } else if (sidecarReducedSinceNs_ == 0) {
+        sidecarReducedSinceNs_ = now;
+      } else if (now - sidecarReducedSinceNs_ > 1'000'000'000ull) {
+        sidecarFallbackCause_ = 2;
+        if (sidecarFallback("the daemon is on its readable-only counter set")) return;
+        sidecarFallbackCause_ = 0;
+      }
     }
     if (sidecarRaw_) {
       sidecarStageRaw();
@@ -517,13 +536,14 @@ void Agent::sidecarStageRaw() {
   sidecarReader_->advance(n);
 }
 
-// The daemon is gone: this process samples its GPU itself from now on.  Its
+// The daemon is gone (or reads only a reduced counter set for this GPU):
+// this process samples its GPU itself from now on.  Its
 // passes were configured at start; here each gets its record layout (one
 // sample, as at an in-process start), its pass-table entry after the
 // daemon's layouts, and pass 0 is left running for samplerLoop.  Kernels
 // already queued only index the daemon's entries, so the table can grow under
 // them.  Returns false (and keeps the sidecar) if the counters cannot start.
-bool Agent::sidecarFallback() {
+bool Agent::sidecarFallback(const char* why) {
   std::string e;
   std::string* err = &e;
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
@@ -578,7 +598,7 @@ bool Agent::sidecarFallback() {
   resetPrev_ = true;  // the first own sample has no interval
   sidecarFallbackNs_ = monoNs();
   sidecarFellBack_ = true;
-  LOG(WARNING) << "GPU agent: the daemon stopped publishing; this process now samples " << pciLocString(pciLoc_)
+  LOG(WARNING) << "GPU agent: " << why << "; this process now samples " << pciLocString(pciLoc_)
                << " itself (" << passes_[0].R << " counter instances)";
   return true;
 }

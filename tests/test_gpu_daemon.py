@@ -622,6 +622,7 @@ def test_sidecar_reports_a_dead_daemon(native_built):
             assert st["sidecar_stale"] is True and st["sidecar_stale_events"] == 1, st
             assert "has not been updated" in c.stderr(), c.tails()
             assert st["sidecar_fell_back"] is True and st["sidecar_fallback_after_ms"] > 0, st
+            assert st["sidecar_fallback_cause"] == "daemon_stale", st
             assert st["last_2s"] > 1500, st  # the job's own 1 kHz after the fallback
             assert st["samples_failed"] == 0 and st["last_error"] == "", st
     finally:
@@ -633,3 +634,47 @@ def test_sidecar_reports_a_dead_daemon(native_built):
                     os.unlink(os.path.join("/dev/shm", f))
                 except OSError:
                     pass
+
+
+def test_sidecar_takes_over_when_the_daemon_reduces_its_set(native_built):
+    """A daemon on the default "auto" set drops to the readable-only `xproc`
+    set while an uncountable job shares the GPU.  A sidecar job on that GPU
+    then samples in process after 1 s (the full set, its own waves' counters),
+    and the daemon keeps reading the readable set beside it: two counting
+    contexts on one GPU leave each other's values alone (profiles/round5/g38)."""
+    flag = os.path.join(tempfile.mkdtemp(prefix="dyred"), "done")
+    env = dict(os.environ)
+    env.pop("ROCP_TOOL_LIBRARIES", None)
+    plain = Child(BUSY, ["90"], env=env)
+    d = None
+    try:
+        plain.wait_ready()
+        d = DaemonProcess(["--enable_gpu_counters", "--gpu_counter_hz=1000"]).start()
+        mon = {}
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            mon = d.rpc({"fn": "getGpuCounterMonitor"})
+            g0 = (mon.get("gpus") or [{}])[0]
+            if mon.get("status") == "ok" and g0.get("sampling") == "xproc" and g0.get("slots_published", 0) > 100:
+                break
+            time.sleep(0.2)
+        assert mon["gpus"][0].get("sampling") == "xproc", mon
+        with Child(SIDECAR_CHILD, args=[flag]) as c:
+            c.wait_ready(180)
+            time.sleep(4.0)  # 1 s on the reduced set, then in-process sampling
+            rc = c.finish(flag, timeout=60)
+            res = [json.loads(l[7:]) for l in c.lines("RESULT ")]
+            assert rc == 0 and res, c.tails()
+            st = res[0]
+            assert st["sidecar_fell_back"] is True and st["sidecar_fallback_cause"] == "reduced_set", st
+            assert st["sidecar_stale_events"] == 0, st
+            assert "readable-only counter set" in c.stderr(), c.tails()
+            assert st["last_2s"] > 1500, st  # the job's own 1 kHz after the takeover
+            assert st["samples_failed"] == 0 and st["last_error"] == "", st
+        after = d.rpc({"fn": "getGpuCounterMonitor"})["gpus"][0]
+        assert after["sampling"] == "xproc" and after["samples"] > mon["gpus"][0]["samples"] + 3000, after
+        assert after.get("sample_failures_total", 0) == 0, after
+    finally:
+        if d is not None:
+            d.stop()
+        plain.kill()
