@@ -447,7 +447,10 @@ class GpuAgent:
         ``counter_passes``: rotate counter configs per pack batch, e.g.
         ``"lite:3,precision:1"`` (3 batches of the lite set, then 1 of the
         precision set: per-precision VALU FLOPs -> fp16/32/64_active, MFMA
-        MOPs by type, VALU busy).  Empty: one pass of ``counter_set``.
+        MOPs by type, VALU busy), or ``"lite:3,mfma:1"`` (the mfma set: matrix
+        ops of every input format, FP8 / FP6-FP4 / INT8 included ->
+        mfma_f8_tflops, mfma_f6f4_tflops, mfma_i8_tops, mfma_tflops).  Empty:
+        one pass of ``counter_set``.
 
         ``gather_scope``: "node" (default: on a multi-node job each node's
         ranks gather to the node's first rank, which logs that node's GPUs)

@@ -24,7 +24,15 @@ PRECISION_COUNTERS = {
     12: "GRBM_GUI_ACTIVE", 13: "GRBM_COUNT",
 }
 P = {n: i for i, n in PRECISION_COUNTERS.items()}
-PASS_MAIN, PASS_PRECISION = 0, 1
+# counters of the "mfma" pass (SlotFormat.h DynoMfmaCounter): every MFMA input format
+MFMA_COUNTERS = {
+    0: "SQ_INSTS_VALU_MFMA_MOPS_F8", 1: "SQ_INSTS_VALU_MFMA_MOPS_F6F4", 2: "SQ_INSTS_VALU_MFMA_MOPS_I8",
+    3: "SQ_VALU_MFMA_BUSY_CYCLES", 4: "SQ_INSTS_VALU_MFMA_MOPS_BF16", 5: "SQ_INSTS_VALU_MFMA_MOPS_F16",
+    6: "SQ_INSTS_VALU_MFMA_MOPS_F32", 7: "SQ_INSTS_VALU_MFMA_MOPS_F64", 8: "TCC_EA0_RDREQ", 9: "TCC_EA0_WRREQ",
+    12: "GRBM_GUI_ACTIVE", 13: "GRBM_COUNT",
+}
+M = {n: i for i, n in MFMA_COUNTERS.items()}
+PASS_MAIN, PASS_PRECISION, PASS_MFMA = 0, 1, 2
 
 DERIVED = [
     "gpu_busy_pct", "mfma_util", "mfma_bf16_tflops", "hbm_read_gbps", "hbm_write_gbps",
@@ -37,6 +45,8 @@ MASK_MAIN = 0x0FFF
 MASK_PRECISION = sum(1 << D[n] for n in ("gpu_busy_pct", "mfma_bf16_tflops", "hbm_read_gbps", "hbm_write_gbps",
                                          "sclk_mhz", "sample_dt_us", "fp16_active", "fp32_active",
                                          "fp64_active", "valu_busy_pct"))
+MASK_MFMA = sum(1 << D[n] for n in ("gpu_busy_pct", "mfma_util", "mfma_bf16_tflops", "hbm_read_gbps",
+                                    "hbm_write_gbps", "sclk_mhz", "sample_dt_us"))
 
 SLOT_FIRST = 0x1
 SLOT_RESET = 0x2
@@ -78,7 +88,7 @@ def reference_pack(raw: np.ndarray, ts_ns: np.ndarray, counter_of: np.ndarray,
 
     raw: [B, R] cumulative per-instance values; counter_of: [R] counter position
     per record (-1 ignored); prev_raw/prev_ts: the sample preceding raw[0];
-    pass_id: which counters the positions hold (PASS_MAIN / PASS_PRECISION)."""
+    pass_id: which counters the positions hold (PASS_MAIN / PASS_PRECISION / PASS_MFMA)."""
     B, R = raw.shape
     n_c = MAX_COUNTERS
     deltas = np.zeros((B, n_c), dtype=np.float64)
@@ -130,6 +140,8 @@ def reference_pack(raw: np.ndarray, ts_ns: np.ndarray, counter_of: np.ndarray,
             derived[b, D["valu_busy_pct"]] = 400 * div(s[P["SQ_ACTIVE_INST_VALU"]], simd_cycles)
             continue
         derived[b, D["mfma_util"]] = 100 * div(s[C["SQ_VALU_MFMA_BUSY_CYCLES"]], simd_cycles)
+        if pass_id == PASS_MFMA:
+            continue  # the per-format MOPs become rates at log time
         derived[b, D["lds_bank_conflict_rate"]] = 100 * div(s[C["SQ_LDS_BANK_CONFLICT"]], s[C["SQ_LDS_IDX_ACTIVE"]])
         derived[b, D["occupancy_pct"]] = 400 * div(s[C["SQ_WAVE_CYCLES"]], gui * k["cu_count"] * 32)
         derived[b, D["waves_per_us"]] = div(s[C["SQ_WAVES"]], dt_us)

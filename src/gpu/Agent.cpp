@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <fstream>
 
@@ -179,6 +180,27 @@ bool Agent::setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::st
   HIP_OK(hipMemcpy(ps.dSegStart, segStart.data(), C * sizeof(int), hipMemcpyHostToDevice), "cp");
   HIP_OK(hipMemcpy(ps.dSegLen, segLen.data(), C * sizeof(int), hipMemcpyHostToDevice), "cp");
   return true;
+}
+
+// "" when the daemon's broadcast can stand in for this process's own
+// sampling: live (heartbeat < 1 s, not paused), on its full set, sampling
+// the counter set and rate this job asked for; else why not.
+std::string Agent::sidecarMismatch(const SlotBroadcastReader& r, const CounterPassSpec& want) const {
+  const auto& h = r.header();
+  char b[200];
+  if (!r.live(monoNs(), 1'000'000'000ull)) return "the daemon's broadcast is not live (stale heartbeat or paused)";
+  if (h.full_set.load() == 0) return "the daemon samples its readable-only set on this GPU";
+  if (std::fabs(h.sample_hz - cfg_.sampleHz) > 0.005 * cfg_.sampleHz) {
+    snprintf(b, sizeof(b), "the daemon samples at %.0f Hz, this job asked for %.0f Hz", h.sample_hz, cfg_.sampleHz);
+    return b;
+  }
+  const uint32_t mask = selectedCounterMask(want.names);
+  if (h.main_pass != want.pass || h.main_counter_mask != mask) {
+    snprintf(b, sizeof(b), "the daemon samples counter set (pass %u, mask 0x%x), this job asked for '%s' (pass %u, mask 0x%x)",
+             h.main_pass, h.main_counter_mask, want.set.c_str(), want.pass, mask);
+    return b;
+  }
+  return "";
 }
 
 bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::string* err) {
@@ -352,16 +374,30 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   sidecarFallbackCause_ = 0;
   sidecarReducedSinceNs_ = 0;
   sampler_ = nullptr;
-  sidecarReader_.reset();
+  {
+    std::lock_guard<std::mutex> g(sidecarMu_);
+    sidecarReader_.reset();
+  }
+  samplerAutoReason_.clear();
+  sidecarDeliveredHz_ = 0.0;
+  sidecarRateLowWindows_ = sidecarReattaches_ = 0;
+  sidecarReattachRefused_ = false;
   if (cfg_.sampler == "auto") {
     // the daemon's cheaper read when it is there for this GPU: a live
-    // broadcast (heartbeat < 1 s, sampling) of the full counter set; this
-    // process reads the counters itself otherwise
+    // broadcast (heartbeat < 1 s, sampling) of the full counter set, at the
+    // rate and with the counter set this job asked for; this process reads
+    // the counters itself otherwise (and says why)
     std::string e;
     const std::string name = cfg_.sidecarRing.empty() ? slotBroadcastName(pciLoc_) : cfg_.sidecarRing;
-    auto r = stepPack_ && cfg_.counterPasses.empty() ? SlotBroadcastReader::open(name, &e) : nullptr;
-    sidecar_ = r && r->live(monoNs(), 1'000'000'000ull) && r->header().full_set.load() != 0;
+    std::unique_ptr<SlotBroadcastReader> r;
+    if (!stepPack_) samplerAutoReason_ = "pack_mode " + cfg_.packMode + " samples in process";
+    else if (!cfg_.counterPasses.empty()) samplerAutoReason_ = "counter_passes rotate sets in process";
+    else if (!(r = SlotBroadcastReader::open(name, &e))) samplerAutoReason_ = e;
+    else samplerAutoReason_ = sidecarMismatch(*r, specs[0]);
+    sidecar_ = r && samplerAutoReason_.empty();
+    if (sidecar_) samplerAutoReason_ = "the daemon's broadcast is live with this job's set and rate";
     cfg_.sampler = sidecar_ ? "daemon" : "agent";
+    LOG(INFO) << "GPU agent: sampler auto -> " << cfg_.sampler << " (" << samplerAutoReason_ << ")";
   }
   if (sidecar_) {
     // the sidecar: the daemon reads the counters; this process only attaches
@@ -369,7 +405,11 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     // and this process's device numbering may differ)
     sidecarName_ = cfg_.sidecarRing.empty() ? slotBroadcastName(pciLoc_) : cfg_.sidecarRing;
     std::string e;
-    sidecarReader_ = SlotBroadcastReader::open(sidecarName_, &e);
+    {
+      auto rd = SlotBroadcastReader::open(sidecarName_, &e);
+      std::lock_guard<std::mutex> g(sidecarMu_);
+      sidecarReader_ = std::move(rd);
+    }
     if (!sidecarReader_) {
       *err = "sampler daemon: " + e + "; start dynolog with --enable_gpu_counters (slot broadcast on) for GPU " +
              pciLocString(pciLoc_);
@@ -1337,7 +1377,10 @@ void Agent::stop() {
   slotProd_.reset();
   slotRing_.reset();  // unlinks the shm segments (the Agent itself is never destroyed)
   if (sampler_) sampler_->stop();
-  sidecarReader_.reset();
+  {
+    std::lock_guard<std::mutex> g(sidecarMu_);
+    sidecarReader_.reset();
+  }
   hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
   hipWarn(hipDeviceSynchronize(), "device sync at stop");
   if (comm_) {
@@ -1516,6 +1559,7 @@ Json Agent::stats() const {
   j["pack_mode"] = cfg_.packMode;
   j["sampler"] = cfg_.sampler;
   j["sampler_requested"] = samplerRequested_;
+  if (!samplerAutoReason_.empty()) j["sampler_auto_reason"] = samplerAutoReason_;
   if (sidecar_) {
     // the daemon reads the counters: its broadcast, and what this agent took
     j["sidecar_ring"] = sidecarName_;
@@ -1532,15 +1576,26 @@ Json Agent::stats() const {
     j["sidecar_fell_back"] = sidecarFellBack_.load();
     if (sidecarFellBack_.load()) {
       j["sidecar_fallback_after_ms"] = (sidecarFallbackNs_.load() - startNs_) * 1e-6;
-      j["sidecar_fallback_cause"] = sidecarFallbackCause_.load() == 2 ? "reduced_set" : "daemon_stale";
+      const int cause = sidecarFallbackCause_.load();
+      j["sidecar_fallback_cause"] = cause == 3 ? "rate_low" : cause == 2 ? "reduced_set" : "daemon_stale";
     }
     j["sidecar_stale_events"] = static_cast<unsigned long long>(sidecarStaleEvents_.load());
     j["sidecar_layouts"] = static_cast<unsigned long long>(sidecarLayouts_.size());
+    // the daemon's delivered rate over the last closed guard window, and the
+    // windows it fell short in (a third takeover cause, "rate_low")
+    j["sidecar_delivered_hz"] = sidecarDeliveredHz_.load();
+    j["sidecar_rate_low_windows"] = static_cast<unsigned long long>(sidecarRateLowWindows_.load());
+    j["sidecar_reattaches"] = static_cast<unsigned long long>(sidecarReattaches_.load());
+    std::lock_guard<std::mutex> g(sidecarMu_);
     if (sidecarReader_) {
       const auto& h = sidecarReader_->header();
       j["sidecar_daemon_pid"] = static_cast<unsigned long long>(h.writer_pid);
       j["sidecar_daemon_hz"] = h.sample_hz;
       j["sidecar_daemon_paused"] = h.paused.load() != 0;
+      char m[16];
+      snprintf(m, sizeof(m), "0x%x", h.main_counter_mask);
+      j["sidecar_daemon_counter_mask"] = m;
+      j["sidecar_daemon_pass"] = h.main_pass;
     }
   }
   j["ring_slots"] = static_cast<unsigned long long>(cfg_.ringSlots);

@@ -281,9 +281,21 @@ class Agent {
   std::atomic<uint64_t> sidecarFallbackNs_{0};
   mutable std::mutex passesMu_;                    // passes_ against stats() while it changes
   bool sidecarFallback(const char* why);           // sampler thread
-  // why it fell back: 1 the daemon stopped publishing, 2 it dropped to its
-  // readable-only set (an uncountable process joined the GPU)
+  // why it fell back: 1 the daemon stopped publishing (or was restarted with
+  // other counter sets), 2 it dropped to its readable-only set (an
+  // uncountable process joined the GPU), 3 it published less than
+  // kSidecarMinRateFraction of its rate over a kSidecarRateWindowNs window
   std::atomic<int> sidecarFallbackCause_{0};
+  static constexpr double kSidecarMinRateFraction = 0.98;
+  static constexpr uint64_t kSidecarRateWindowNs = 2'000'000'000ull;
+  BroadcastRateGuard sidecarGuard_;                // sampler thread
+  std::atomic<double> sidecarDeliveredHz_{0.0};   // the daemon's rate over the last closed window
+  std::atomic<uint64_t> sidecarRateLowWindows_{0}, sidecarReattaches_{0};
+  bool sidecarReattachRefused_ = false;            // sampler thread: warned once
+  mutable std::mutex sidecarMu_;                   // sidecarReader_ swaps (re-attach) against stats()
+  bool sidecarReattach(uint64_t now);              // sampler thread: a restarted daemon's new segment
+  std::string sidecarMismatch(const SlotBroadcastReader& r, const CounterPassSpec& want) const;
+  std::string samplerAutoReason_;                  // sampler "auto": why it chose what it chose
   uint64_t sidecarReducedSinceNs_ = 0;             // sampler thread
   std::atomic<uint64_t> sidecarStaleEvents_{0};    // outages seen
   void sidecarStageRaw();        // one pass over the new raw samples (sampler thread)

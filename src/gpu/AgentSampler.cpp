@@ -371,10 +371,14 @@ void Agent::sidecarLoop() {
   bool wasPaused = false;
   const uint64_t tick = 1'000'000;  // 1 ms: the daemon's rate is at most 1 kHz per GPU
   uint64_t next = monoNs();
+  uint64_t lastReopenCheck = 0;
+  bool rateWarned = false;
+  sidecarGuard_ = BroadcastRateGuard(sidecarReader_->header().sample_hz, kSidecarMinRateFraction, kSidecarRateWindowNs);
   while (!stopFlag_) {
     if (paused_ || hold_.held()) {
       hold_.acknowledgeParked();
       wasPaused = true;
+      sidecarGuard_.reset();
       usleep(2000);
       next = monoNs();
       continue;
@@ -388,15 +392,24 @@ void Agent::sidecarLoop() {
     phaseHist_[phaseHistN_ % kPhaseHist] = {now, hPhase_ ? __atomic_load_n(hPhase_, __ATOMIC_ACQUIRE) : 0u};
     ++phaseHistN_;
     if (flushReq_.load() != flushAck_.load()) flushAck_ = flushReq_.load();
+    const uint64_t hb = sidecarReader_->header().heartbeat_ns.load(std::memory_order_relaxed);
+    const uint64_t hbAge = hb == 0 || now < hb ? 0 : now - hb;
+    // A restarted daemon unlinks the old segment and publishes a new one under
+    // the same name: this reader's heartbeat never moves again.  Once the
+    // heartbeat is late, look for a new segment every 250 ms and re-attach
+    // (same counter layouts: the staged entries keep their meaning).
+    if (hbAge > 500'000'000ull && now - lastReopenCheck > 250'000'000ull) {
+      lastReopenCheck = now;
+      if (sidecarReattach(now)) continue;
+    }
     // failure detection: a daemon that stopped publishing (killed, hung)
     // leaves a stale heartbeat; say so once per outage (stats sidecar_stale)
-    const uint64_t hb = sidecarReader_->header().heartbeat_ns.load(std::memory_order_relaxed);
-    const bool stale = hb == 0 || now < hb ? false : now - hb > 3'000'000'000ull;
+    const bool stale = hbAge > 3'000'000'000ull;
     if (stale && !sidecarStale_.exchange(true)) {
       sidecarStaleEvents_++;
       LOG(WARNING) << "GPU agent: the daemon's broadcast " << sidecarName_ << " has not been updated for "
-                   << (now - hb) / 1000000 << " ms (writer pid " << sidecarReader_->header().writer_pid << ")"
-                   << (fallbackPasses_.empty() ? "; no counter samples until it resumes"
+                   << hbAge / 1000000 << " ms (writer pid " << sidecarReader_->header().writer_pid << ")"
+                   << (fallbackPasses_.empty() ? "; no counter samples until it resumes or restarts"
                                                : "; sampling the GPU in this process from now on");
       // take the GPU's sampling over: the thread continues as samplerLoop
       sidecarFallbackCause_ = 1;
@@ -420,6 +433,29 @@ void Agent::sidecarLoop() {
         sidecarFallbackCause_ = 2;
         if (sidecarFallback("the daemon is on its readable-only counter set")) return;
         sidecarFallbackCause_ = 0;
+      }
+    }
+    // The daemon is live but slow: what it published over the last window
+    // (not what this process staged) against its own target rate.  One
+    // daemon reading 8 GPUs could serialise its reads inside the runtime and
+    // deliver, say, 600/s per GPU with a fresh heartbeat; then this process
+    // samples its GPU itself.
+    const bool daemonPaused = sidecarReader_->header().paused.load(std::memory_order_relaxed) != 0;
+    if (sidecarGuard_.tick(now, sidecarReader_->head(), daemonPaused || stale)) {
+      sidecarDeliveredHz_.store(sidecarGuard_.lastRateHz(), std::memory_order_relaxed);
+      if (sidecarGuard_.low()) {
+        sidecarRateLowWindows_++;
+        char why[160];
+        snprintf(why, sizeof(why), "the daemon delivered %.1f samples/s of its %.0f over %.0f s",
+                 sidecarGuard_.lastRateHz(), sidecarGuard_.targetHz(), kSidecarRateWindowNs * 1e-9);
+        if (!fallbackPasses_.empty()) {
+          sidecarFallbackCause_ = 3;
+          if (sidecarFallback(why)) return;
+          sidecarFallbackCause_ = 0;
+        } else if (!rateWarned) {
+          rateWarned = true;
+          LOG(WARNING) << "GPU agent: " << why << " (no in-process fallback armed)";
+        }
       }
     }
     if (sidecarRaw_) {
@@ -474,6 +510,42 @@ void Agent::sidecarLoop() {
       next = t;
     }
   }
+}
+
+// A new segment under the broadcast's name (the daemon was restarted): attach
+// to it when it is live and samples the layouts this process's pass table was
+// built from (raw), or at all (slots).  A restarted daemon with other sets
+// cannot feed the staged pass indices: the armed fallback takes over instead.
+bool Agent::sidecarReattach(uint64_t now) {
+  if (!sidecarReader_->replaced()) return false;
+  std::string e;
+  auto r = SlotBroadcastReader::open(sidecarName_, &e);
+  if (!r || !r->live(now, 1'000'000'000ull)) return false;  // not publishing yet: look again later
+  if (sidecarRaw_ && (!r->carriesRaw() || !r->sameLayouts(*sidecarReader_))) {
+    if (!sidecarReattachRefused_) {
+      sidecarReattachRefused_ = true;
+      LOG(WARNING) << "GPU agent: the restarted daemon (pid " << r->header().writer_pid << ") samples other counter "
+                   << "layouts on " << sidecarName_ << "; not re-attaching";
+    }
+    if (!fallbackPasses_.empty()) {
+      sidecarFallbackCause_ = 1;
+      if (sidecarFallback("the restarted daemon samples other counter sets")) return true;
+      sidecarFallbackCause_ = 0;
+    }
+    return false;
+  }
+  r->skipToHead();
+  {
+    std::lock_guard<std::mutex> g(sidecarMu_);
+    sidecarReader_ = std::move(r);
+  }
+  sidecarHaveLast_ = false;  // the next staged sample has no predecessor
+  sidecarStale_ = false;
+  sidecarGuard_ = BroadcastRateGuard(sidecarReader_->header().sample_hz, kSidecarMinRateFraction, kSidecarRateWindowNs);
+  sidecarReattaches_++;
+  LOG(WARNING) << "GPU agent: re-attached to the restarted daemon's broadcast " << sidecarName_ << " (writer pid "
+               << sidecarReader_->header().writer_pid << ")";
+  return true;
 }
 
 // Raw sidecar: the daemon's raw samples go into the staging ring as if this
@@ -545,46 +617,69 @@ void Agent::sidecarStageRaw() {
 // them.  Returns false (and keeps the sidecar) if the counters cannot start.
 bool Agent::sidecarFallback(const char* why) {
   std::string e;
-  std::string* err = &e;
-  hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
   const uint32_t base = static_cast<uint32_t>(sidecarLayouts_.size());
-  std::vector<DynoStepPass> t(fallbackPasses_.size());
-  // uploads on a private non-blocking stream: the null stream would queue
-  // them behind the trainer's work (seconds of run-ahead, profiles/round5/g30)
-  hipStream_t copy = nullptr;
-  HIP_OK(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking), "fallback stream");
-  struct StreamGuard {
-    hipStream_t s;
-    ~StreamGuard() { (void)hipStreamDestroy(s); }
-  } guard{copy};
-  for (size_t i = fallbackPasses_.size(); i-- > 0;) {
-    PassState& ps = fallbackPasses_[i];
-    ps.sampler->select();
-    bool ok = ps.sampler->start(err);
-    std::vector<double> vals(ps.R);
-    std::vector<uint64_t> ids(ps.R);
-    size_t n = ps.R;
-    ok = ok && ps.sampler->sample(vals.data(), &n, ids.data(), err) && n == ps.R && setupLayout(ps, ids, err, copy);
-    if (!ok) {
-      ps.sampler->stop();
-      LOG(ERROR) << "GPU agent: in-process fallback failed (" << e << "); waiting for the daemon";
-      std::lock_guard<std::mutex> g(passesMu_);
-      fallbackPasses_.clear();
-      return false;
+  // every pass started so far, stopped again if the takeover fails part-way
+  std::vector<PassState*> started;
+  auto attempt = [&](std::string* err) -> bool {
+    hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
+    std::vector<DynoStepPass> t(fallbackPasses_.size());
+    // uploads on a private non-blocking stream: the null stream would queue
+    // them behind the trainer's work (seconds of run-ahead, profiles/round5/g30)
+    hipStream_t copy = nullptr;
+    HIP_OK(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking), "fallback stream");
+    struct StreamGuard {
+      hipStream_t s;
+      ~StreamGuard() { (void)hipStreamDestroy(s); }
+    } guard{copy};
+    for (size_t i = fallbackPasses_.size(); i-- > 0;) {
+      PassState& ps = fallbackPasses_[i];
+      ps.sampler->select();
+      if (!ps.sampler->start(err)) return false;
+      started.push_back(&ps);
+      std::vector<double> vals(ps.R);
+      std::vector<uint64_t> ids(ps.R);
+      size_t n = ps.R;
+      if (!ps.sampler->sample(vals.data(), &n, ids.data(), err)) return false;
+      if (n != ps.R) {
+        *err = "sample returned " + std::to_string(n) + " records, expected " + std::to_string(ps.R);
+        return false;
+      }
+      if (!setupLayout(ps, ids, err, copy)) return false;
+      if (i > 0) {
+        ps.sampler->stop();
+        started.pop_back();
+      }
+      t[i].perm = ps.dPerm;
+      t[i].seg_start = ps.dSegStart;
+      t[i].seg_len = ps.dSegLen;
+      t[i].k = ps.consts;
+      t[i].R = static_cast<int32_t>(ps.R);
+      t[i].n_counters = DC_NUM_COUNTERS;
+      t[i].pass = ps.spec.pass;
+      t[i].counter_mask = ps.counterMask;
     }
-    if (i > 0) ps.sampler->stop();
-    t[i].perm = ps.dPerm;
-    t[i].seg_start = ps.dSegStart;
-    t[i].seg_len = ps.dSegLen;
-    t[i].k = ps.consts;
-    t[i].R = static_cast<int32_t>(ps.R);
-    t[i].n_counters = DC_NUM_COUNTERS;
-    t[i].pass = ps.spec.pass;
-    t[i].counter_mask = ps.counterMask;
+    HIP_OK(hipMemcpyAsync(dStepPasses_ + base, t.data(), t.size() * sizeof(DynoStepPass), hipMemcpyHostToDevice,
+                          copy),
+           "fallback pass table");
+    HIP_OK(hipStreamSynchronize(copy), "fallback pass table sync");
+    return true;
+  };
+  if (!attempt(&e)) {
+    // one cleanup for every failure: no counting context left programmed,
+    // no device layout left behind, and no second attempt (the takeover is
+    // one-shot; the job keeps the daemon's samples while it has them)
+    for (PassState* ps : started) ps->sampler->stop();
+    for (auto& ps : fallbackPasses_) {
+      for (int** d : {&ps.dPerm, &ps.dSegStart, &ps.dSegLen}) {
+        if (*d) hipWarn(hipFree(*d), "hipFree fallback layout");
+        *d = nullptr;
+      }
+    }
+    LOG(ERROR) << "GPU agent: in-process fallback failed (" << e << "); staying on the daemon's broadcast";
+    std::lock_guard<std::mutex> g(passesMu_);
+    fallbackPasses_.clear();
+    return false;
   }
-  HIP_OK(hipMemcpyAsync(dStepPasses_ + base, t.data(), t.size() * sizeof(DynoStepPass), hipMemcpyHostToDevice, copy),
-         "fallback pass table");
-  HIP_OK(hipStreamSynchronize(copy), "fallback pass table sync");
   {
     std::lock_guard<std::mutex> g(passesMu_);
     passes_ = std::move(fallbackPasses_);

@@ -161,7 +161,9 @@ struct CounterPassSpec {
 // "lite:3,precision:1" -> lite for 3 batches, then precision for 1, repeat.
 // "" -> a single pass of defaultSet.  Sets: full | lite | lean | core (main
 // pass), precision (per-precision VALU FLOPs, MFMA MOPs by type, VALU busy,
-// plus TCC + GRBM), or a '+'-joined list of main-pass counter names.
+// plus TCC + GRBM), mfma (MFMA MOPs of every input format -- FP8, FP6/FP4,
+// INT8, BF16, F16, F32, F64 -- MFMA busy, TCC + GRBM), or a '+'-joined list
+// of main-pass counter names.
 // delta[] positions a pass selected (non-empty names), as a bit mask
 unsigned selectedCounterMask(const std::vector<std::string>& names);
 
