@@ -37,6 +37,10 @@ class SmiApi {
   // optional entry points (older libraries may lack them: RSMI_STATUS_NOT_SUPPORTED)
   rsmi_status_t eccEnabledBlocks(uint32_t dv, uint64_t* mask);
   rsmi_status_t pcieReplayCount(uint32_t dv, uint64_t* count);
+  // PCIe packets sent / received over one second and the max payload size
+  // (the driver's pcie_bw file; blocks ~1 s).  NOT_SUPPORTED on MI355X
+  // (profiles/round6/g01): no directional PCIe source there.
+  rsmi_status_t pcieThroughput(uint32_t dv, uint64_t* sent, uint64_t* received, uint64_t* maxPktBytes);
   rsmi_status_t xgmiErrorStatus(uint32_t dv, rsmi_xgmi_status_t* status);
   rsmi_status_t numaNode(uint32_t dv, uint32_t* node);
   rsmi_status_t linkType(uint32_t a, uint32_t b, uint64_t* hops, RSMI_IO_LINK_TYPE* type);
@@ -73,6 +77,7 @@ class SmiApi {
   rsmi_status_t (*rsmi_status_string_)(rsmi_status_t, const char**) = nullptr;
   rsmi_status_t (*rsmi_dev_ecc_enabled_get_)(uint32_t, uint64_t*) = nullptr;
   rsmi_status_t (*rsmi_dev_pci_replay_counter_get_)(uint32_t, uint64_t*) = nullptr;
+  rsmi_status_t (*rsmi_dev_pci_throughput_get_)(uint32_t, uint64_t*, uint64_t*, uint64_t*) = nullptr;
   rsmi_status_t (*rsmi_dev_xgmi_error_status_)(uint32_t, rsmi_xgmi_status_t*) = nullptr;
 };
 

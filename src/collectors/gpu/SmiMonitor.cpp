@@ -157,10 +157,11 @@ void logSmiRecord(Logger& log, int device, const SmiSample* prev, const SmiSampl
       log.logFloat("pcie_bandwidth_gbps", static_cast<float>(gbps));
       uint64_t bytes = static_cast<uint64_t>(gbps * 1e9 * dtS);
       log.logUint("pcie_bytes", bytes);
-      if (aliases) {
-        log.logUint("pcie_tx_bytes", bytes / 2);
-        log.logUint("pcie_rx_bytes", bytes / 2);
-      }
+    }
+    if (aliases && cur.pcieDirValid && dtS > 0) {
+      // DCGM fields 1009 / 1010 (DcgmGroupInfo.cpp:46-47): bytes per direction
+      log.logUint("pcie_tx_bytes", static_cast<uint64_t>(static_cast<double>(cur.pcieTxBytesPerS) * dtS));
+      log.logUint("pcie_rx_bytes", static_cast<uint64_t>(static_cast<double>(cur.pcieRxBytesPerS) * dtS));
     }
     if (cur.accumulationCounter > prev->accumulationCounter) {
       double d = double(cur.accumulationCounter - prev->accumulationCounter);
@@ -169,6 +170,10 @@ void logSmiRecord(Logger& log, int device, const SmiSample* prev, const SmiSampl
       log.logFloat("thermal_violation_pct",
                    static_cast<float>(100.0 * double(cur.thmResidencyAcc - prev->thmResidencyAcc) / d));
     }
+  }
+  if (aliases && !cur.pcieDirValid) {
+    // no directional source: never a made-up split of the total
+    log.logStr("metrics_unavailable", "pcie_tx_bytes,pcie_rx_bytes");
   }
   log.logInt("num_processes", static_cast<int64_t>(cur.pids.size()));
   for (const auto& [k, v] : attribution) log.logStr(k, v);
@@ -235,6 +240,24 @@ bool SmiMonitor::readDevice(int dev, SmiSample* o) {
   api.renderMinor(d, &o->renderMinor);
   api.hiveId(d, &o->hiveId);
   readHealth(dev, o);
+  // directional PCIe bytes, where the GPU has them (probed once per device)
+  if (pcieDir_.size() != static_cast<size_t>(numDevices_)) pcieDir_.assign(static_cast<size_t>(numDevices_), -1);
+  int& dir = pcieDir_[static_cast<size_t>(dev)];
+  if (dir != 0) {
+    uint64_t sent = 0, recv = 0, mps = 0;
+    const rsmi_status_t st = api.pcieThroughput(d, &sent, &recv, &mps);
+    if (st == RSMI_STATUS_SUCCESS && mps > 0) {
+      o->pcieDirValid = true;
+      o->pcieTxBytesPerS = sent * mps;
+      o->pcieRxBytesPerS = recv * mps;
+      if (dir < 0) LOG(INFO) << "GPU " << dev << ": directional PCIe bytes from rsmi_dev_pci_throughput_get";
+      dir = 1;
+    } else if (dir < 0) {
+      LOG(INFO) << "GPU " << dev << ": no directional PCIe source (rsmi_dev_pci_throughput_get: "
+                << SmiApi::statusString(st) << "); pcie_tx_bytes / pcie_rx_bytes are not logged";
+      dir = 0;
+    }
+  }
   return true;
 }
 

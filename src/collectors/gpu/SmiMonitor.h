@@ -5,7 +5,10 @@
 // DcgmGroupInfo::log, DcgmGroupInfo.cpp:348-368).  Keys:
 //   reference-compatible: gpu_device_utilization, gpu_memory_utilization,
 //     gpu_power_draw, gpu_frequency_mhz, minor_id, graphics_engine_active_ratio,
-//     hbm_mem_bw_util, pcie_{tx,rx}_bytes (acc delta), nvlink_{rx,tx}_bytes ->
+//     hbm_mem_bw_util, pcie_{tx,rx}_bytes (only from a directional source:
+//     rsmi_dev_pci_throughput_get, which MI355X does not support -- then the
+//     record lists them under metrics_unavailable and carries the total
+//     pcie_bytes / pcie_bandwidth_gbps instead), nvlink_{rx,tx}_bytes ->
 //     xgmi_{rx,tx}_bytes, job_id/username/slurm_account/slurm_partition,
 //     smi_error (the dcgm_error analogue)
 //   AMD-native: gfx_activity, umc_activity, socket_power, gfxclk_mhz,
@@ -45,6 +48,10 @@ struct SmiSample {
   uint16_t tempHotspot = 0, tempMem = 0;
   uint64_t vramUsed = 0, vramTotal = 0;
   uint64_t pcieBwAcc = 0;            // GB/s accumulator (pmfw units)
+  // directional PCIe rate (rsmi_dev_pci_throughput_get: packets per second x
+  // the max payload size, an upper bound), when the GPU supports it
+  bool pcieDirValid = false;
+  uint64_t pcieTxBytesPerS = 0, pcieRxBytesPerS = 0;
   uint64_t xgmiReadKb[8] = {}, xgmiWriteKb[8] = {};
   uint64_t accumulationCounter = 0, pptResidencyAcc = 0, thmResidencyAcc = 0;
   uint64_t throttleStatus = 0;
@@ -101,6 +108,7 @@ class SmiMonitor {
   void readHealth(int dev, SmiSample* out);
   int numDevices_ = 0;
   std::vector<uint64_t> eccMask_;        // per device: RAS blocks still queried
+  std::vector<int> pcieDir_;             // per device: -1 not probed, 0 unsupported, 1 read
   std::map<int, uint64_t> injectedUc_;   // --fault_inject=ecc_uc
   SampleFn sampleFn_;
   std::vector<SmiSample> prev_, cur_;
