@@ -372,12 +372,14 @@ def test_bench_overhead_matrix_helpers():
     spec.loader.exec_module(bench)
     # entries sample in process unless they name the daemon sidecar
     ag = ["--sampler", "agent"]
-    assert bench.matrix_entries("core, lean,core:3/lite:1,lite@hz500@b128@kb,lite@daemon@dslots") == [
+    assert bench.matrix_entries("core, lean,core:3/lite:1,lite@hz500@b128@kb,lite@daemon@host") == [
         ("core", "core", "", ag), ("lean", "lean", "", ag), ("core:3/lite:1", "lite", "core:3,lite:1", ag),
         ("lite@hz500@b128@kb", "lite", "", ag + ["--sample-hz", "500.0", "--pack-batch", "128", "--kernel-breakdown"]),
-        ("lite@daemon@dslots", "lite", "", ["--sampler", "daemon", "--sidecar-slots"])]
+        ("lite@daemon@host", "lite", "", ["--sampler", "daemon", "--pack-mode", "host"])]
     with pytest.raises(SystemExit):
         bench.matrix_entries("lite@x1")
+    with pytest.raises(SystemExit):  # retired in round 6
+        bench.matrix_entries("lite@device")
     # the sidecar daemon's CPU time (utime + stime of all its threads)
     assert bench.proc_cpu_s(os.getpid()) > 0 and bench.proc_cpu_s(2 ** 30) is None
     # overhead = 0.1 % + 0.5 % per million instance reads / s
