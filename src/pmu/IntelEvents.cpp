@@ -1,5 +1,6 @@
 #include "pmu/IntelEvents.h"
 
+#include <array>
 #include <cstring>
 
 #include "common/System.h"
@@ -188,6 +189,29 @@ struct IntelNamedTable {
   size_t n;
 };
 #include "pmu/IntelNamedEvents.inc"
+
+struct IntelUncoreEvent {
+  const char* pmu;  // sysfs PMU prefix: uncore_<box>, instances uncore_<box>_<n>
+  const char* name;
+  const char* fields;
+};
+struct IntelUncoreTable {
+  const char* family;
+  const IntelUncoreEvent* events;
+  size_t n;
+};
+#include "pmu/IntelUncoreEvents.inc"
+
+// the sysfs PMU `dev` is an instance of uncore box `prefix` (uncore_cha_3 of
+// uncore_cha; uncore_pcu of itself)
+bool uncoreInstanceOf(const std::string& dev, const std::string& prefix) {
+  if (dev == prefix) return true;
+  if (dev.size() <= prefix.size() + 1 || dev.compare(0, prefix.size(), prefix) != 0 || dev[prefix.size()] != '_')
+    return false;
+  for (size_t i = prefix.size() + 1; i < dev.size(); ++i)
+    if (dev[i] < '0' || dev[i] > '9') return false;
+  return true;
+}
 }  // namespace
 
 const char* intelNamedFamily(CpuArch arch) {
@@ -216,6 +240,52 @@ std::vector<std::pair<std::string, std::string>> intelNamedEvents(const std::str
     if (family == t.family)
       for (size_t i = 0; i < t.n; ++i) out.emplace_back(t.events[i].name, t.events[i].fields);
   return out;
+}
+
+const char* intelUncoreFamily(CpuArch arch, int stepping) {
+  // model 0x55: Skylake-SP steppings 0-4, Cascade Lake 5-7 (the reference's
+  // skylakex / cascadelakex uncore tables, JsonEvents.h:135+)
+  if (arch == CpuArch::IntelSkylakeX) return stepping >= 5 ? "clx" : "skx";
+  return intelNamedFamily(arch);
+}
+
+std::vector<std::array<std::string, 3>> intelUncoreEvents(const std::string& family) {
+  std::vector<std::array<std::string, 3>> out;
+  for (const auto& t : kIntelUncoreTables)
+    if (family == t.family)
+      for (size_t i = 0; i < t.n; ++i) out.push_back({t.events[i].pmu, t.events[i].name, t.events[i].fields});
+  return out;
+}
+
+int registerIntelUncoreEvents(PmuDeviceManager& mgr) {
+  const char* fam = intelUncoreFamily(mgr.arch(), mgr.cpuInfo().stepping);
+  if (!fam) return 0;
+  int added = 0;
+  std::vector<PmuDevice> updated;
+  for (const auto& [devName, dev] : mgr.devices()) {
+    if (devName.rfind("uncore_", 0) != 0) continue;
+    PmuDevice d = dev;
+    int n = 0;
+    for (const auto& t : kIntelUncoreTables) {
+      if (std::string(fam) != t.family) continue;
+      for (size_t i = 0; i < t.n; ++i) {
+        const IntelUncoreEvent& e = t.events[i];
+        if (!uncoreInstanceOf(devName, e.pmu) || d.aliases.count(e.name)) continue;
+        bool encodable = true;
+        for (const auto& kv : split(e.fields, ','))
+          if (!d.format.count(kv.substr(0, kv.find('=')))) encodable = false;
+        if (!encodable) continue;
+        d.aliases[e.name] = e.fields;
+        ++n;
+      }
+    }
+    if (n) {
+      updated.push_back(std::move(d));
+      added += n;
+    }
+  }
+  for (auto& d : updated) mgr.addDevice(std::move(d));
+  return added;
 }
 
 int registerIntelEvents(PmuDeviceManager& mgr) {
@@ -252,7 +322,8 @@ int registerIntelEvents(PmuDeviceManager& mgr) {
       added += n;
     }
   }
-  return added;
+  // and every uncore box's named events (IntelUncoreEvents.inc)
+  return added + registerIntelUncoreEvents(mgr);
 }
 
 int intelIssueSlots(CpuArch arch) {

@@ -8,6 +8,7 @@
 // tables matter only for mixed fleets.
 #pragma once
 
+#include <array>
 #include <string>
 #include <utility>
 #include <vector>
@@ -28,6 +29,16 @@ int registerIntelEvents(PmuDeviceManager& mgr);
 // (lower-case name, perf format fields) events.
 const char* intelNamedFamily(CpuArch arch);
 std::vector<std::pair<std::string, std::string>> intelNamedEvents(const std::string& family);
+// The generated uncore catalog (src/pmu/IntelUncoreEvents.inc, the reference's
+// 16 *_uncore_* tables): the family of an arch + stepping (Skylake-SP 0-4 /
+// Cascade Lake 5-7 share model 0x55) and its {PMU prefix, name, fields}.
+const char* intelUncoreFamily(CpuArch arch, int stepping);
+std::vector<std::array<std::string, 3>> intelUncoreEvents(const std::string& family);
+// Adds those names as aliases on every sysfs instance of their box
+// (uncore_cha_0 .. uncore_cha_<n>, uncore_imc_<n>, uncore_pcu, ...) whose
+// format encodes them; returns how many were added (registerIntelEvents
+// calls it).
+int registerIntelUncoreEvents(PmuDeviceManager& mgr);
 // Issue width for the level-1 topdown slot count.
 int intelIssueSlots(CpuArch arch);
 bool isIntelArch(CpuArch arch);

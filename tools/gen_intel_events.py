@@ -2,7 +2,9 @@
 """Generates src/pmu/IntelNamedEvents.inc: the named core-PMU events of every
 Intel family the reference ships tables for, as one compact line each
 (name -> perf "event=..,umask=..[,cmask=..][,inv=1][,edge=1][,any=1]"
-[,offcore_rsp=..|,ldlat=..]).
+[,offcore_rsp=..|,ldlat=..]), and src/pmu/IntelUncoreEvents.inc: the named
+uncore events of its 16 uncore tables (CHA / CBox, IMC, M2M, M3UPI, UPI /
+QPI, IIO, IRP, PCU, UBox, ...), one line each (PMU prefix, name, perf fields).
 
 The encodings are Intel's public perfmon data, which the reference carries as
 generated C++ (/root/reference/hbt/src/perf_event/json_events/generated/intel/
@@ -14,7 +16,7 @@ writes the table the daemon compiles in.  Run it again only to change the
 selection:
 
     python3 tools/gen_intel_events.py /root/reference/hbt/src/perf_event/json_events/generated/intel \\
-        src/pmu/IntelNamedEvents.inc
+        src/pmu/IntelNamedEvents.inc src/pmu/IntelUncoreEvents.inc
 """
 import os
 import re
@@ -36,6 +38,24 @@ FAMILIES = {
     "goldmont_core": "glm",
     "snowridgex_core": "snr",
     "knightslanding_core": "knl",
+}
+
+# reference uncore table stem -> family key (experimental tables merge into theirs)
+UNCORE_FAMILIES = {
+    "skylakex_uncore": "skx",
+    "skylakex_uncore_experimental": "skx",
+    "cascadelakex_uncore": "clx",
+    "cascadelakex_uncore_experimental": "clx",
+    "icelake_uncore": "icl",
+    "skylake_uncore": "skl",
+    "broadwellx_uncore": "bdx",
+    "broadwell_uncore": "bdw",
+    "broadwellde_uncore": "bdwde",
+    "haswellx_uncore": "hsx",
+    "ivybridge_uncore": "ivb",
+    "sandybridge_uncore": "snb",
+    "snowridgex_uncore": "snr",
+    "knightslanding_uncore": "knl",
 }
 
 EVENT_RE = re.compile(
@@ -70,7 +90,72 @@ def encoding(body: str):
     return ",".join(parts), code
 
 
-def main(src_dir: str, out_path: str) -> int:
+def uncore_encoding(body: str):
+    """perf fields of an uncore event, or None when it needs a filter MSR
+    (CHA / CBox filters, PCU band thresholds) this table cannot express."""
+    msr = re.search(r"\.msr_values\s*=\s*\{([^}]*)\}", body)
+    if msr and any(int(v, 0) for v in msr.group(1).split(",") if v.strip()):
+        return None
+    f = {k: v.strip() for k, v in FIELD_RE.findall(re.sub(r"\.msr_values\s*=\s*\{[^}]*\}", "", body))}
+    code = int(f.get("code", "0"), 0)
+    umask = int(f.get("umask", "0"), 0)
+    parts = [f"event=0x{code:02x}"]
+    if umask:
+        parts.append(f"umask=0x{umask:02x}")
+    cmask = int(f.get("cmask", "0"), 0)
+    if cmask:
+        parts.append(f"thresh=0x{cmask:x}")  # the uncore PMUs' threshold field
+    for flag in ("inv", "edge"):
+        if f.get(flag) == "true":
+            parts.append(f"{flag}=1")
+    return ",".join(parts)
+
+
+def write_uncore(src_dir: str, out_path: str) -> int:
+    tables = {}
+    for fn in sorted(os.listdir(src_dir)):
+        stem = re.sub(r"_v[\d_]+(_experimental)?\.cpp$", lambda m: m.group(1) or "", fn)
+        if stem not in UNCORE_FAMILIES or not fn.endswith(".cpp"):
+            continue
+        with open(os.path.join(src_dir, fn)) as f:
+            text = f.read()
+        fam = UNCORE_FAMILIES[stem]
+        files, rows, seen, skipped = tables.setdefault(fam, ([], [], set(), [0]))
+        files.append(fn)
+        for pmu, name, body, brief in EVENT_RE.findall(text):
+            if not pmu.startswith("uncore_"):
+                continue
+            enc = uncore_encoding(body)
+            if enc is None:
+                skipped[0] += 1
+                continue
+            key = (pmu, name.lower())
+            if key in seen:
+                continue
+            seen.add(key)
+            rows.append((pmu, name.lower(), enc))
+    with open(out_path, "w") as out:
+        out.write("// Generated by tools/gen_intel_events.py from Intel's public perfmon uncore\n"
+                  "// event encodings (as carried by the reference's generated tables,\n"
+                  "// /root/reference/hbt/src/perf_event/json_events/generated/intel/*_uncore_*.cpp).\n"
+                  "// {PMU prefix (sysfs uncore_<box>[_<n>]), event name, perf fields}; events that\n"
+                  "// need a filter MSR are left out.  Do not edit: re-run the generator.\n")
+        for fam, (files, rows, _, skipped) in sorted(tables.items()):
+            out.write(f"\n// {', '.join(files)}: {len(rows)} uncore events ({skipped[0]} need a filter MSR)\n")
+            out.write(f"static const IntelUncoreEvent kIntelUncore_{fam}[] = {{\n")
+            for pmu, name, enc in rows:
+                out.write(f'    {{"{pmu}", "{name}", "{enc}"}},\n')
+            out.write("};\n")
+        out.write("\nstatic const IntelUncoreTable kIntelUncoreTables[] = {\n")
+        for fam in sorted(tables):
+            out.write(f'    {{"{fam}", kIntelUncore_{fam}, sizeof(kIntelUncore_{fam}) / sizeof(kIntelUncore_{fam}[0])}},\n')
+        out.write("};\n")
+    n = sum(len(t[1]) for t in tables.values())
+    print(f"{out_path}: {n} uncore events in {len(tables)} families")
+    return 0
+
+
+def main(src_dir: str, out_path: str, uncore_path: str = "") -> int:
     tables = {}
     for fn in sorted(os.listdir(src_dir)):
         stem = re.sub(r"_v[\d_]+\.cpp$", "", fn)
@@ -107,8 +192,10 @@ def main(src_dir: str, out_path: str) -> int:
             out.write(f'    {{"{fam}", kIntel_{fam}, sizeof(kIntel_{fam}) / sizeof(kIntel_{fam}[0])}},\n')
         out.write("};\n")
     print(f"{out_path}: {sum(len(r) for _, r in tables.values())} events in {len(tables)} families")
+    if uncore_path:
+        write_uncore(src_dir, uncore_path)
     return 0
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1], sys.argv[2]))
+    sys.exit(main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else ""))
