@@ -663,7 +663,8 @@ def test_long_step_grows_the_staging_ring(native_built):
     """A 10 s step at 1 kHz (no step() call for 10 s: gradient accumulation,
     a big model) against a 2048-entry staging ring: the ring grows on a
     helper thread whenever half of it waits for a step, so not one tick is
-    lost and the next step() packs all ~10,000 samples."""
+    lost and the next step() packs all ~10,000 samples (its payload carries
+    gather_cap_slots of them, the next steps the rest)."""
     res = _run("""
         from dynolog_amd import agent
         agent.preinit()
@@ -679,17 +680,22 @@ def test_long_step_grows_the_staging_ring(native_built):
                 y = x @ x
             torch.cuda.synchronize()
         t1 = agent.mono_ns()
-        a.pack_pending(); a.step(); torch.cuda.synchronize(); a.flush()
+        a.pack_pending(); a.step(); torch.cuda.synchronize()
+        packed_at_first_step = a.stats()["step_packed"]
+        for _ in range(3):  # the backlog beyond one payload
+            a.step(); torch.cuda.synchronize()
+        a.flush()
         time.sleep(0.3)
         st = a.stats(); wc = a.window_counts(t0, t1)
         a.stop()
-        print("RESULT " + json.dumps(dict(stats=st, wc=wc, window_s=(t1 - t0) * 1e-9)))
+        print("RESULT " + json.dumps(dict(stats=st, wc=wc, window_s=(t1 - t0) * 1e-9, first=packed_at_first_step)))
     """, timeout=300)
     st = res["stats"]
     print(json.dumps({k: v for k, v in st.items() if k.startswith("step_") or k in ("samples_taken", "late_ticks")}))
     assert st["step_stage_full_ticks"] == 0, st
     assert st["step_stage_grows"] >= 2 and st["step_stage_slots"] >= 16384, st
     assert st["step_stage_grow_failures"] == 0 and st["samples_failed"] == 0, st
+    assert res["first"] >= 0.995 * 1000 * res["window_s"], res["first"]  # one step packed them all
     # every sample of the window reached the aggregator (1 kHz, none dropped)
     assert res["wc"][0] >= 0.995 * 1000 * res["window_s"], res["wc"]
     assert st["ranks"][0]["received"] >= res["wc"][0] and st["ranks"][0]["dropped"] == 0, st

@@ -707,14 +707,18 @@ def test_sidecar_takeover_survives_the_uncountable_job_leaving(native_built):
             c.wait_ready(180)
             time.sleep(4.0)  # the takeover
             plain.kill()
+            # back to the full set -- unless this pytest process itself holds the
+            # GPU (an earlier in-process test initialised HIP): then it stays an
+            # uncountable process on the GPU and the daemon stays on xproc
+            want = "xproc" if _runner_holds_gpu() else "lite"
             deadline = time.time() + 30
             g0 = {}
             while time.time() < deadline:
                 g0 = d.rpc({"fn": "getGpuCounterMonitor"})["gpus"][0]
-                if g0.get("sampling") == "lite":
+                if g0.get("sampling") == want and plain.p.pid not in (g0.get("compute_pids") or []):
                     break
                 time.sleep(0.2)
-            assert g0.get("sampling") == "lite", g0
+            assert g0.get("sampling") == want, g0
             before = g0["samples"]
             time.sleep(3.0)
             rc = c.finish(flag, timeout=60)
@@ -726,7 +730,7 @@ def test_sidecar_takeover_survives_the_uncountable_job_leaving(native_built):
             assert st["samples_failed"] == 0 and st["last_error"] == "", st
             assert st["sample_latency_us_max"] < 100_000, st
         after = d.rpc({"fn": "getGpuCounterMonitor"})["gpus"][0]
-        assert after["sampling"] == "lite" and after["samples"] > before + 2500, after
+        assert after["sampling"] == want and after["samples"] > before + 2500, after
         assert after.get("sample_failures_total", 0) == 0, after
     finally:
         if d is not None:
