@@ -392,7 +392,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     sidecarReader_.reset();
   }
   samplerAutoReason_.clear();
-  sidecarDeliveredHz_ = 0.0;
+  sidecarDeliveredHz_ = -1.0;
   sidecarRateLowWindows_ = sidecarReattaches_ = 0;
   sidecarReattachRefused_ = false;
   if (cfg_.sampler == "auto") {
@@ -1571,7 +1571,9 @@ Json Agent::stats() const {
     j["sidecar_layouts"] = static_cast<unsigned long long>(sidecarLayouts_.size());
     // the daemon's delivered rate over the last closed guard window, and the
     // windows it fell short in (a third takeover cause, "rate_low")
-    j["sidecar_delivered_hz"] = sidecarDeliveredHz_.load();
+    // (null until a window has closed: a run shorter than one window)
+    const double deliveredHz = sidecarDeliveredHz_.load();
+    j["sidecar_delivered_hz"] = deliveredHz < 0.0 ? Json(nullptr) : Json(deliveredHz);
     j["sidecar_rate_low_windows"] = static_cast<unsigned long long>(sidecarRateLowWindows_.load());
     j["sidecar_reattaches"] = static_cast<unsigned long long>(sidecarReattaches_.load());
     std::lock_guard<std::mutex> g(sidecarMu_);

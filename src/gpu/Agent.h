@@ -310,7 +310,7 @@ class Agent {
   static constexpr double kSidecarMinRateFraction = 0.98;
   static constexpr uint64_t kSidecarRateWindowNs = 2'000'000'000ull;
   BroadcastRateGuard sidecarGuard_;                // sampler thread
-  std::atomic<double> sidecarDeliveredHz_{0.0};   // the daemon's rate over the last closed window
+  std::atomic<double> sidecarDeliveredHz_{-1.0};  // the daemon's rate over the last closed window (<0: none yet)
   std::atomic<uint64_t> sidecarRateLowWindows_{0}, sidecarReattaches_{0};
   bool sidecarReattachRefused_ = false;            // sampler thread: warned once
   mutable std::mutex sidecarMu_;                   // sidecarReader_ swaps (re-attach) against stats()

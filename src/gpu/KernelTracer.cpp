@@ -162,6 +162,23 @@ bool KernelTracer::stop(std::string* err) {
   windowEnd_ = monoNow();
   active_ = false;
   auto f = rocprofiler_flush_buffer(rocprofiler_buffer_id_t{buffer_});
+  // The runtime completes a dispatch's record on its own thread: a kernel
+  // the caller already synchronised on can still be on its way into the
+  // buffer at this flush (one GEMM of ten missing from a window, round 6
+  // g03).  Flush again until no record arrived for 20 ms, at most 250 ms.
+  const uint64_t t0 = monoNow();
+  size_t seen = records().size();
+  uint64_t quietSince = t0;
+  while (f == ROCPROFILER_STATUS_SUCCESS && monoNow() - t0 < 250'000'000ull &&
+         monoNow() - quietSince < 20'000'000ull) {
+    usleep(2000);
+    f = rocprofiler_flush_buffer(rocprofiler_buffer_id_t{buffer_});
+    const size_t n = records().size();
+    if (n != seen) {
+      seen = n;
+      quietSince = monoNow();
+    }
+  }
   if (s != ROCPROFILER_STATUS_SUCCESS || f != ROCPROFILER_STATUS_SUCCESS) {
     if (err) *err = "stop kernel trace: " + rpErr(s != ROCPROFILER_STATUS_SUCCESS ? s : f);
     return false;
