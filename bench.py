@@ -749,9 +749,14 @@ def _main(args, wd) -> int:
                                          "--gpu_counter_reporting_interval_s=3600"]).start()
                 deadline = time.time() + 60
                 mon = {}
-                while time.time() < deadline:  # every GPU's thread publishing slots
+                while time.time() < deadline:
+                    # every GPU's thread publishing slots, for a full second: its
+                    # broadcast then names the rate it holds, and each rank's
+                    # agent (sampler "auto") refuses a GPU's broadcast that runs
+                    # short from the start
                     mon = sidecar.rpc({"fn": "getGpuCounterMonitor"}) or {}
-                    if mon.get("status") == "ok" and all(g.get("slots_published", 0) > 0 for g in mon.get("gpus", [{}])):
+                    if mon.get("status") == "ok" and all(g.get("slots_published", 0) > 0 and g.get("sample_hz_achieved", 0) > 0
+                                                         for g in mon.get("gpus", [{}])):
                         break
                     time.sleep(0.2)
                 else:

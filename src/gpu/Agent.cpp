@@ -195,6 +195,11 @@ std::string Agent::sidecarMismatch(const SlotBroadcastReader& r, const CounterPa
     snprintf(b, sizeof(b), "the daemon samples at %.0f Hz, this job asked for %.0f Hz", h.sample_hz, cfg_.sampleHz);
     return b;
   }
+  const uint64_t mhz = h.rate_mhz.load(std::memory_order_relaxed);
+  if (mhz != 0 && static_cast<double>(mhz) < 1000.0 * kSidecarMinRateFraction * h.sample_hz) {
+    snprintf(b, sizeof(b), "the daemon held %.1f samples/s of its %.0f over its last second", mhz * 1e-3, h.sample_hz);
+    return b;
+  }
   const uint32_t mask = selectedCounterMask(want.names);
   if (h.main_pass != want.pass || h.main_counter_mask != mask) {
     snprintf(b, sizeof(b), "the daemon samples counter set (pass %u, mask 0x%x), this job asked for '%s' (pass %u, mask 0x%x)",

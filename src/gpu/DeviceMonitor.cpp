@@ -380,6 +380,10 @@ void DeviceMonitor::loop(Gpu* g) {
       }
       prevTs = 0;  // the first sample after a pause has no interval
       paused = false;
+      {
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->rateT0 = 0;  // the rate window restarts: a pause is not a shortfall
+      }
       next = monoNs();
     }
     if (auto_ && g->wantAlt.load(std::memory_order_relaxed) != g->onAlt) {
@@ -403,6 +407,7 @@ void DeviceMonitor::loop(Gpu* g) {
       hostPack(cur.data(), prev.data(), R, p.counterOf.data(), t1, prevTs, static_cast<uint32_t>(t1 - t0), seq++,
                static_cast<uint32_t>(g->index), p.consts, &s, p.spec.pass);
       s.counter_mask = selectedCounterMask(p.spec.names);
+      double rateNow = -1.0;  // a rate window closed with this sample
       DynoGatherHeader h{};
       h.count = 1;
       h.device = g->index;
@@ -421,9 +426,11 @@ void DeviceMonitor::loop(Gpu* g) {
           g->rateHz = static_cast<double>(g->samplesOk - g->rateN0) * 1e9 / static_cast<double>(t1 - g->rateT0);
           g->rateT0 = t1;
           g->rateN0 = g->samplesOk;
+          rateNow = g->rateHz;
         }
       }
       if (g->bcast) {
+        if (rateNow >= 0.0) g->bcast->setAchievedRate(rateNow);
         if (g->bcast->carriesRaw()) {
           // the raw sample as the job's step kernel wants it (its previous
           // sample is the previous entry, zeros, or none)

@@ -76,7 +76,11 @@ struct SlotBroadcastHeader {
   // selectedCounterMask): an agent takes the sidecar only for its own set
   uint32_t main_pass;
   uint32_t main_counter_mask;
-  uint64_t reserved[18];
+  // the rate the writer held over its last second of sampling, milli-Hz
+  // (0: not a full second yet): an agent refuses a broadcast that already
+  // runs short at start-up instead of finding out over its first window
+  std::atomic<uint64_t> rate_mhz;
+  uint64_t reserved[17];
 };
 
 // One counter layout of the writer (a counter set): entry i of a raw sample
@@ -257,6 +261,9 @@ class SlotBroadcastWriter {
     hdr_->paused.store(paused ? 1u : 0u, std::memory_order_relaxed);
   }
   void setFullSet(bool full) { hdr_->full_set.store(full ? 1u : 0u, std::memory_order_relaxed); }
+  void setAchievedRate(double hz) {
+    hdr_->rate_mhz.store(hz > 0.0 ? static_cast<uint64_t>(hz * 1000.0 + 0.5) : 0u, std::memory_order_relaxed);
+  }
   void setMainSet(uint32_t pass, uint32_t counterMask) {
     hdr_->main_pass = pass;
     hdr_->main_counter_mask = counterMask;

@@ -276,6 +276,20 @@ TEST(DevMon, SlowReadTripsTheRateGuardForThatGpuOnly) {
   EXPECT_GT(gpus[2].at("late_ticks").asInt(), 0);
   EXPECT_LT(gpus[2].at("sample_hz_achieved").asDouble(), 700.0);
   EXPECT_GE(gpus[0].at("sample_hz_achieved").asDouble(), 1000.0 * healthyFraction());
+  // the same rates in each broadcast's header (milli-Hz), where a starting
+  // agent with sampler "auto" reads them
+  for (int i : {0, 2}) {
+    std::string e;
+    auto r = SlotBroadcastReader::open(names[i], &e);
+    ASSERT_TRUE(r);
+    const double hz = static_cast<double>(r->header().rate_mhz.load()) * 1e-3;
+    if (i == 2) {
+      EXPECT_GT(hz, 400.0);
+      EXPECT_LT(hz, 700.0);
+    } else {
+      EXPECT_GE(hz, 1000.0 * healthyFraction());
+    }
+  }
   m.stop();
 }
 
