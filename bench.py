@@ -1185,6 +1185,10 @@ def _main(args, wd) -> int:
                     # delivered rate as this rank measured it
                     "sidecar_fallback_cause": st.get("sidecar_fallback_cause"),
                     "sidecar_delivered_hz": st.get("sidecar_delivered_hz"),
+                    # takeovers and hand-backs (the rank samples in process now
+                    # when the first exceeds the second)
+                    "sidecar_takeovers": st.get("sidecar_takeovers"),
+                    "sidecar_handbacks": st.get("sidecar_handbacks"),
                     "gather_latency_us_avg": round(st.get("gather_latency_us_avg", 0.0), 2),
                     "gathers": st.get("gathers")}
             ranks = [None] * env.world
@@ -1208,7 +1212,8 @@ def _main(args, wd) -> int:
                              "step_staged", "collective", "sidecar_raw", "sidecar_layouts", "sidecar_stale",
                              "sidecar_fell_back", "sidecar_fallback_after_ms", "sidecar_fallback_cause",
                              "sidecar_delivered_hz", "sidecar_rate_low_windows", "sidecar_reattaches",
-                             "sampler_auto_reason", "step_stage_slots", "step_stage_grows")
+                             "sampler_auto_reason", "step_stage_slots", "step_stage_grows",
+                             "sidecar_takeovers", "sidecar_handbacks")
                             if k in agent_stats}
             out["agent"]["host_rss_mb_after_warmup"] = rss_start
         if args.sampler == "daemon" and env.local_rank == 0:

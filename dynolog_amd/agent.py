@@ -424,7 +424,7 @@ class GpuAgent:
               comm_init_timeout_ms: int = 60000, pack_mode: str = "step",
               pin_threads: bool = True, step_stage_slots: int = 8192, step_stage_max_bytes: int = 2 << 30,
               sampler: str = "agent", sidecar_ring: str = "", sidecar_raw: bool = True,
-              sidecar_fallback: bool = True) -> "GpuAgent":
+              sidecar_fallback: bool = True, sidecar_handback: bool = True) -> "GpuAgent":
         """Start sampling this rank's GPU. For world > 1 the RCCL unique id is
         created on rank 0 and broadcast over ``process_group`` (default group)
         unless ``uid`` is given.
@@ -489,7 +489,12 @@ class GpuAgent:
         agent when the daemon stops publishing for 3 s, drops to its
         readable-only set, or delivers less than 98 % of its rate over 2 s
         (stats ``sidecar_fallback_cause``).  A restarted daemon sampling the
-        same sets is re-attached to instead.  With sampler "auto" the daemon
+        same sets is re-attached to instead.  ``sidecar_handback`` (default):
+        after a takeover, once the daemon's broadcast (or a restarted
+        daemon's, same sets) has been live, on its full set and at 98 % of its
+        rate for 3 s (doubling with each hand-back), this process stops its
+        own context and samples through the daemon again (stats
+        ``sidecar_takeovers``, ``sidecar_handbacks``).  With sampler "auto" the daemon
         is taken only when its broadcast is live, on the full set, at this
         job's ``sample_hz`` and ``counter_set`` (stats ``sampler_auto_reason``)."""
         if not _preinit_done:
@@ -530,6 +535,8 @@ class GpuAgent:
             cfg["sidecar_raw"] = False
         if not sidecar_fallback:
             cfg["sidecar_fallback"] = False
+        if not sidecar_handback:
+            cfg["sidecar_handback"] = False
         if counter_passes:
             cfg["counter_passes"] = counter_passes
         if labels is not None:
@@ -577,7 +584,7 @@ class GpuAgent:
                                   comm_init_timeout_ms=comm_init_timeout_ms, pack_mode=pack_mode,
                                   pin_threads=pin_threads, step_stage_slots=step_stage_slots,
                                   step_stage_max_bytes=step_stage_max_bytes, sampler=sampler, sidecar_ring=sidecar_ring, sidecar_raw=sidecar_raw,
-                                  sidecar_fallback=sidecar_fallback)
+                                  sidecar_fallback=sidecar_fallback, sidecar_handback=sidecar_handback)
                 # report the mode that was asked for; a chained fallback (RCCL,
                 # then the mailbox) keeps every reason, first failure first
                 inner = agent.config.get("fallback_reason")

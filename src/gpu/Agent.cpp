@@ -69,6 +69,7 @@ AgentConfig AgentConfig::fromJson(const Json& j) {
   if (j.contains("sidecar_ring")) c.sidecarRing = j.at("sidecar_ring").asString();
   if (j.contains("sidecar_raw") && !j.at("sidecar_raw").asBool()) c.sidecarSlotCopy = true;
   if (j.contains("sidecar_fallback")) c.sidecarFallback = j.at("sidecar_fallback").asBool();
+  if (j.contains("sidecar_handback")) c.sidecarHandBack = j.at("sidecar_handback").asBool();
   if (j.contains("log_file")) c.logFile = j.at("log_file").asString();
   if (j.contains("daemon_endpoint")) c.daemonEndpoint = j.at("daemon_endpoint").asString();
   if (j.contains("pin_threads")) c.pinThreads = j.at("pin_threads").asBool();
@@ -386,8 +387,12 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   if (specs.empty()) return false;
   passes_.clear();
   fallbackPasses_.clear();
+  retiredPasses_.clear();
   passIdxBase_ = 0;
   sidecarFellBack_ = false;
+  handBackGate_ = HandBackGate();
+  sidecarTakeovers_ = sidecarHandBacks_ = 0;
+  sidecarHandBackHoldNs_ = handBackGate_.holdNs();
   sidecarFallbackNs_ = 0;
   sidecarFallbackCause_ = 0;
   sidecarReducedSinceNs_ = 0;
@@ -726,9 +731,17 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   samplerDone_ = consumerDone_ = ctlDone_ = false;
   hold_.resetAcknowledged();  // no hold is pending (start() refuses while one is held)
   samplerThread_ = std::thread([this] {
-    if (sidecar_) sidecarLoop();
-    // the daemon died and this process took over its GPU's sampling
-    if (!sidecar_ || sidecarFellBack_.load()) samplerLoop();
+    if (!sidecar_) {
+      samplerLoop();
+    } else {
+      // the sidecar: the daemon's broadcast, or this process's own sampling
+      // after a takeover (sidecarLoop returns), and back again after a
+      // hand-back (samplerLoop returns); either returns at stop
+      while (!stopFlag_) {
+        if (sidecarFellBack_.load()) samplerLoop();
+        else sidecarLoop();
+      }
+    }
     samplerDone_ = true;
   });
   if (root) {
@@ -1424,10 +1437,12 @@ void Agent::releaseDevice() {
   hRing_ = nullptr;
   dHdr_ = nullptr;
   dRing_ = nullptr;
-  for (auto& ps : passes_) {
-    freeDev(ps.dPerm);
-    freeDev(ps.dSegStart);
-    freeDev(ps.dSegLen);
+  for (auto* v : {&passes_, &fallbackPasses_, &retiredPasses_}) {  // (a handed-back job's passes keep their layouts)
+    for (auto& ps : *v) {
+      freeDev(ps.dPerm);
+      freeDev(ps.dSegStart);
+      freeDev(ps.dSegLen);
+    }
   }
   freeDev(dStepPasses_);
   for (auto& l : sidecarLayouts_) {
@@ -1566,8 +1581,13 @@ Json Agent::stats() const {
       std::lock_guard<std::mutex> g(passesMu_);  // the fallback moves these on the sampler thread
       j["sidecar_fallback_armed"] = !fallbackPasses_.empty() || sidecarFellBack_.load();
     }
+    // sampling in process now (after a takeover, before a hand-back)
     j["sidecar_fell_back"] = sidecarFellBack_.load();
-    if (sidecarFellBack_.load()) {
+    j["sidecar_takeovers"] = static_cast<unsigned long long>(sidecarTakeovers_.load());
+    j["sidecar_handbacks"] = static_cast<unsigned long long>(sidecarHandBacks_.load());
+    j["sidecar_handback"] = cfg_.sidecarHandBack;
+    j["sidecar_handback_hold_ms"] = sidecarHandBackHoldNs_.load() * 1e-6;
+    if (sidecarTakeovers_.load() > 0) {  // the latest takeover
       j["sidecar_fallback_after_ms"] = (sidecarFallbackNs_.load() - startNs_) * 1e-6;
       const int cause = sidecarFallbackCause_.load();
       j["sidecar_fallback_cause"] = cause == 3 ? "rate_low" : cause == 2 ? "reduced_set" : "daemon_stale";

@@ -93,6 +93,8 @@ struct AgentConfig {
   bool sidecarFallback = true;       // raw sidecar: when the daemon's heartbeat is > 3 s old,
                                      // sample the GPU in this process from then on (its
                                      // counting context is configured: preinit)
+  bool sidecarHandBack = true;       // after a takeover: sample through the daemon again once its
+                                     // broadcast has been healthy for a hold (3 s, doubling)
   bool sidecarSlotCopy = false;      // "sidecar_raw": false asked for the retired slot copy
   uint64_t stepStageSlots = 8192;    // pack_mode step: staged samples between steps at start
                                      // (power of 2; 8 s at 1 kHz, ~35 MiB pinned for 528
@@ -295,13 +297,22 @@ class Agent {
   // (after the daemon's layouts) at the fallback; the sampler thread then
   // continues as samplerLoop with staging pass_idx offset by passIdxBase_.
   std::vector<PassState> fallbackPasses_;
+  std::vector<PassState> retiredPasses_;  // a failed second takeover's: layouts freed at stop
   int agentIdx_ = -1;
   uint32_t passIdxBase_ = 0;
   int stepPassCount_ = 1;                          // entries of dStepPasses_
   std::atomic<bool> sidecarFellBack_{false};
   std::atomic<uint64_t> sidecarFallbackNs_{0};
   mutable std::mutex passesMu_;                    // passes_ against stats() while it changes
-  bool sidecarFallback(const char* why);           // sampler thread
+  bool sidecarFallback(const char* why, int cause);  // sampler thread; cause: sidecarFallbackCause_
+  // The way back: a job that took over samples through the daemon again once
+  // its broadcast (or a restarted daemon's, same layouts) has been live, on
+  // its full set and at 98 % of its rate for HandBackGate's hold; the passes
+  // return to fallbackPasses_ with their layouts, for the next takeover.
+  bool sidecarHandBack(uint64_t now);              // sampler thread (in samplerLoop)
+  HandBackGate handBackGate_;                      // sampler thread
+  std::atomic<uint64_t> sidecarTakeovers_{0}, sidecarHandBacks_{0};
+  std::atomic<uint64_t> sidecarHandBackHoldNs_{0};
   // why it fell back: 1 the daemon stopped publishing (or was restarted with
   // other counter sets), 2 it dropped to its readable-only set (an
   // uncountable process joined the GPU), 3 it published less than

@@ -228,6 +228,7 @@ void Agent::samplerLoop() {
   int staged = 0;
   std::string err;
   bool wasPaused = false;
+  uint64_t lastHandBackCheck = 0;
   while (!stopFlag_) {
     if (paused_ || hold_.held()) {
       if (staged > 0 && !stepPack_) {  // (step packing stages every sample at once)
@@ -261,6 +262,13 @@ void Agent::samplerLoop() {
         staged = 0;
       }
       flushAck_ = req;
+    }
+    if (sidecarFellBack_.load(std::memory_order_relaxed) && cfg_.sidecarHandBack) {
+      const uint64_t now = monoNs();
+      if (now - lastHandBackCheck >= 500'000'000ull) {
+        lastHandBackCheck = now;
+        if (sidecarHandBack(now)) return;  // the thread continues as sidecarLoop
+      }
     }
     // step packing: the next staging entry, once no launch may still read it
     // (entries [stepDone_ - 1, head) are the in-flight launches' and the next
@@ -432,7 +440,10 @@ void Agent::sidecarLoop() {
     // (same counter layouts: the staged entries keep their meaning).
     if (hbAge > 500'000'000ull && now - lastReopenCheck > 250'000'000ull) {
       lastReopenCheck = now;
-      if (sidecarReattach(now)) continue;
+      if (sidecarReattach(now)) {
+        if (sidecarFellBack_.load()) return;  // the restarted daemon's sets differ: took over
+        continue;
+      }
     }
     // failure detection: a daemon that stopped publishing (killed, hung)
     // leaves a stale heartbeat; say so once per outage (stats sidecar_stale)
@@ -444,9 +455,7 @@ void Agent::sidecarLoop() {
                    << (fallbackPasses_.empty() ? "; no counter samples until it resumes or restarts"
                                                : "; sampling the GPU in this process from now on");
       // take the GPU's sampling over: the thread continues as samplerLoop
-      sidecarFallbackCause_ = 1;
-      if (!fallbackPasses_.empty() && sidecarFallback("the daemon stopped publishing")) return;
-      sidecarFallbackCause_ = 0;
+      if (!fallbackPasses_.empty() && sidecarFallback("the daemon stopped publishing", 1)) return;
     } else if (!stale && hb != 0 && sidecarStale_.exchange(false)) {
       LOG(INFO) << "GPU agent: the daemon's broadcast " << sidecarName_ << " is live again";
     }
@@ -462,9 +471,7 @@ void Agent::sidecarLoop() {
       } else if (sidecarReducedSinceNs_ == 0) {
         sidecarReducedSinceNs_ = now;
       } else if (now - sidecarReducedSinceNs_ > 1'000'000'000ull) {
-        sidecarFallbackCause_ = 2;
-        if (sidecarFallback("the daemon is on its readable-only counter set")) return;
-        sidecarFallbackCause_ = 0;
+        if (sidecarFallback("the daemon is on its readable-only counter set", 2)) return;
       }
     }
     // The daemon is live but slow: what it published over the last window
@@ -482,9 +489,7 @@ void Agent::sidecarLoop() {
         snprintf(why, sizeof(why), "the daemon delivered %.1f samples/s of its %.0f over %.0f s",
                  sidecarGuard_.lastRateHz(), sidecarGuard_.targetHz(), kSidecarRateWindowNs * 1e-9);
         if (!fallbackPasses_.empty()) {
-          sidecarFallbackCause_ = 3;
-          if (sidecarFallback(why)) return;
-          sidecarFallbackCause_ = 0;
+          if (sidecarFallback(why, 3)) return;
         } else if (!rateWarned) {
           rateWarned = true;
           LOG(WARNING) << "GPU agent: " << why << " (no in-process fallback armed)";
@@ -519,9 +524,7 @@ bool Agent::sidecarReattach(uint64_t now) {
                    << "layouts on " << sidecarName_ << "; not re-attaching";
     }
     if (!fallbackPasses_.empty()) {
-      sidecarFallbackCause_ = 1;
-      if (sidecarFallback("the restarted daemon samples other counter sets")) return true;
-      sidecarFallbackCause_ = 0;
+      if (sidecarFallback("the restarted daemon samples other counter sets", 1)) return true;
     }
     return false;
   }
@@ -604,13 +607,23 @@ void Agent::sidecarStageRaw() {
 // daemon's layouts, and pass 0 is left running for samplerLoop.  Kernels
 // already queued only index the daemon's entries, so the table can grow under
 // them.  Returns false (and keeps the sidecar) if the counters cannot start.
-bool Agent::sidecarFallback(const char* why) {
+bool Agent::sidecarFallback(const char* why, int cause) {
   std::string e;
   const uint32_t base = static_cast<uint32_t>(sidecarLayouts_.size());
   // every pass started so far, stopped again if the takeover fails part-way
   std::vector<PassState*> started;
+  // a takeover after a hand-back: the passes kept their layouts and their
+  // pass-table entries; only pass 0's context starts again
+  const bool ready = !fallbackPasses_.empty() && fallbackPasses_[0].dPerm != nullptr;
   auto attempt = [&](std::string* err) -> bool {
     hipWarn(hipSetDevice(cfg_.device), "hipSetDevice");
+    if (ready) {
+      PassState& p0 = fallbackPasses_[0];
+      p0.sampler->select();
+      if (!p0.sampler->start(err)) return false;
+      started.push_back(&p0);
+      return true;
+    }
     std::vector<DynoStepPass> t(fallbackPasses_.size());
     // uploads on a private non-blocking stream: the null stream would queue
     // them behind the trainer's work (seconds of run-ahead, profiles/round5/g30)
@@ -658,14 +671,20 @@ bool Agent::sidecarFallback(const char* why) {
     // no device layout left behind, and no second attempt (the takeover is
     // one-shot; the job keeps the daemon's samples while it has them)
     for (PassState* ps : started) ps->sampler->stop();
-    for (auto& ps : fallbackPasses_) {
-      for (int** d : {&ps.dPerm, &ps.dSegStart, &ps.dSegLen}) {
-        if (*d) hipWarn(hipFree(*d), "hipFree fallback layout");
-        *d = nullptr;
-      }
-    }
     LOG(ERROR) << "GPU agent: in-process fallback failed (" << e << "); staying on the daemon's broadcast";
     std::lock_guard<std::mutex> g(passesMu_);
+    if (ready) {
+      // samples staged before the hand-back may still wait for a step kernel
+      // that reads these layouts: they are freed at stop
+      for (auto& ps : fallbackPasses_) retiredPasses_.push_back(std::move(ps));
+    } else {
+      for (auto& ps : fallbackPasses_) {
+        for (int** d : {&ps.dPerm, &ps.dSegStart, &ps.dSegLen}) {
+          if (*d) hipWarn(hipFree(*d), "hipFree fallback layout");
+          *d = nullptr;
+        }
+      }
+    }
     fallbackPasses_.clear();
     return false;
   }
@@ -681,9 +700,59 @@ bool Agent::sidecarFallback(const char* why) {
   passIdxBase_ = base;
   resetPrev_ = true;  // the first own sample has no interval
   sidecarFallbackNs_ = monoNs();
+  sidecarFallbackCause_ = cause;
+  sidecarTakeovers_++;
+  handBackGate_.reset();
   sidecarFellBack_ = true;
   LOG(WARNING) << "GPU agent: " << why << "; this process now samples " << pciLocString(pciLoc_)
                << " itself (" << passes_[0].R << " counter instances)";
+  return true;
+}
+
+// After a takeover (samplerLoop, every 500 ms): is the daemon healthy again?
+// Its broadcast -- or a restarted daemon's new segment with the same layouts,
+// which the pass table's daemon entries still describe -- must be live
+// (heartbeat < 200 ms, not paused), on its full set and at >= 98 % of its
+// rate over its last second, at every check for the gate's hold.  Then this
+// process stops its own context and returns to staging the daemon's samples;
+// the passes go back to fallbackPasses_ with their layouts and pass-table
+// entries, so a later takeover only restarts pass 0.  A daemon that stays
+// slow (rate_low) or keeps its reduced set never passes the gate.
+bool Agent::sidecarHandBack(uint64_t now) {
+  if (sidecarReader_->replaced()) {
+    std::string e;
+    auto r = SlotBroadcastReader::open(sidecarName_, &e);
+    if (!r || !r->carriesRaw() || !r->sameLayouts(*sidecarReader_) || !r->live(now, 200'000'000ull)) {
+      handBackGate_.observe(now, false);
+      return false;
+    }
+    std::lock_guard<std::mutex> g(sidecarMu_);
+    sidecarReader_ = std::move(r);
+    sidecarReattaches_++;
+  }
+  const auto& h = sidecarReader_->header();
+  const uint64_t mhz = h.rate_mhz.load(std::memory_order_relaxed);
+  const bool healthy = sidecarReader_->live(now, 200'000'000ull) && h.full_set.load(std::memory_order_relaxed) != 0 &&
+                       mhz != 0 && static_cast<double>(mhz) >= 1000.0 * kSidecarMinRateFraction * h.sample_hz;
+  if (!handBackGate_.observe(now, healthy)) return false;
+  sampler_->stop();
+  {
+    std::lock_guard<std::mutex> g(passesMu_);
+    fallbackPasses_ = std::move(passes_);
+    passes_.clear();
+  }
+  sampler_ = nullptr;
+  curPass_ = 0;
+  batchesInPass_ = 0;
+  sidecarReader_->skipToHead();  // what the daemon sampled meanwhile, this process sampled too
+  sidecarHaveLast_ = false;      // the next staged sample has no predecessor
+  sidecarStale_ = false;
+  sidecarReducedSinceNs_ = 0;
+  sidecarHandBacks_++;
+  sidecarHandBackHoldNs_ = handBackGate_.holdNs();
+  sidecarFellBack_ = false;
+  LOG(WARNING) << "GPU agent: the daemon's broadcast " << sidecarName_ << " is healthy again (writer pid "
+               << h.writer_pid << ", " << mhz * 1e-3 << " samples/s); sampling through it again";
   return true;
 }
 

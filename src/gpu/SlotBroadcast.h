@@ -443,6 +443,38 @@ class SlotBroadcastReader {
 // over from a daemon whose broadcast is live but slow (8 GPUs' reads
 // serialising inside one daemon would otherwise cost the job its rate
 // silently: the heartbeat stays fresh).
+// When may a job that took its GPU's sampling over hand it back to the
+// daemon?  Once the broadcast has looked healthy (live, on its full set, at
+// its rate) at every check for holdNs; each hand-back doubles the hold for
+// the next one (up to maxHoldNs), so a daemon that keeps failing costs the
+// job a few switches, not a flapping sampler.
+class HandBackGate {
+ public:
+  explicit HandBackGate(uint64_t holdNs = 3'000'000'000ull, uint64_t maxHoldNs = 120'000'000'000ull)
+      : hold_(holdNs), maxHold_(maxHoldNs) {}
+  void reset() { since_ = 0; }  // a takeover: the hold starts over
+  // true when the broadcast has been healthy for the whole hold: hand back now
+  bool observe(uint64_t nowNs, bool healthy) {
+    if (!healthy || nowNs < since_) {
+      since_ = 0;
+      return false;
+    }
+    if (since_ == 0) {
+      since_ = nowNs;
+      return false;
+    }
+    if (nowNs - since_ < hold_) return false;
+    since_ = 0;
+    hold_ = std::min(hold_ * 2, maxHold_);
+    return true;
+  }
+  uint64_t holdNs() const { return hold_; }  // the next hand-back's
+
+ private:
+  uint64_t hold_, maxHold_;
+  uint64_t since_ = 0;
+};
+
 class BroadcastRateGuard {
  public:
   explicit BroadcastRateGuard(double hz = 1000.0, double minFraction = 0.98, uint64_t windowNs = 2'000'000'000ull)

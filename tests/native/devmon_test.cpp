@@ -470,3 +470,34 @@ TEST(DevMon, RateGuardWindows) {
   EXPECT_EQ(g.windows(), 3u);
   EXPECT_EQ(g.lowWindows(), 1u);
 }
+
+// The hand-back gate: a job that took over returns to the daemon only after
+// the broadcast has been healthy at every check for the hold; one unhealthy
+// check restarts it; each hand-back doubles the next hold, up to the cap.
+TEST(DevMon, HandBackGateHoldsAndBacksOff) {
+  const uint64_t s = 1'000'000'000ull;
+  HandBackGate g(3 * s, 10 * s);
+  uint64_t t = 100 * s;
+  EXPECT_FALSE(g.observe(t, true));  // the hold starts
+  EXPECT_FALSE(g.observe(t + 2 * s, true));
+  EXPECT_FALSE(g.observe(t + 2 * s + s / 2, false));  // unhealthy: starts over
+  EXPECT_FALSE(g.observe(t + 3 * s, true));
+  EXPECT_FALSE(g.observe(t + 5 * s, true));
+  EXPECT_TRUE(g.observe(t + 6 * s, true));  // 3 s healthy
+  EXPECT_EQ(g.holdNs(), 6 * s);
+  t += 20 * s;
+  g.reset();  // the next takeover
+  EXPECT_FALSE(g.observe(t, true));
+  EXPECT_FALSE(g.observe(t + 5 * s, true));
+  EXPECT_TRUE(g.observe(t + 6 * s, true));
+  EXPECT_EQ(g.holdNs(), 10 * s);  // capped
+  t += 20 * s;
+  EXPECT_FALSE(g.observe(t, true));
+  EXPECT_FALSE(g.observe(t + 9 * s, true));
+  EXPECT_TRUE(g.observe(t + 10 * s, true));
+  EXPECT_EQ(g.holdNs(), 10 * s);
+  // a clock that goes backwards (a reset timestamp) never hands back early
+  EXPECT_FALSE(g.observe(t + 30 * s, true));
+  EXPECT_FALSE(g.observe(t + 29 * s, true));
+  EXPECT_FALSE(g.observe(t + 30 * s, true));
+}
