@@ -676,6 +676,7 @@ def test_sidecar_hands_back_to_a_restarted_daemon(native_built):
             res = [json.loads(l[7:]) for l in c.lines("RESULT ")]
             assert rc == 0 and res, c.tails()
             st = res[0]
+            print(json.dumps({k: v for k, v in st.items() if k.startswith("sidecar_") or k == "last_2s"}))
             assert st["sidecar_takeovers"] == 1 and st["sidecar_fallback_cause"] == "daemon_stale", st
             assert st["sidecar_handbacks"] == 1 and st["sidecar_fell_back"] is False, st
             assert st["sidecar_reattaches"] == 1 and st["sidecar_daemon_pid"] == d2.proc.pid, st
@@ -784,6 +785,8 @@ def test_sidecar_takeover_survives_the_uncountable_job_leaving(native_built):
             res = [json.loads(l[7:]) for l in c.lines("RESULT ")]
             assert rc == 0 and res, c.tails()
             st = res[0]
+            print(json.dumps({"want": want, **{k: v for k, v in st.items()
+                                               if k.startswith("sidecar_") or k == "last_2s"}}))
             assert st["sidecar_takeovers"] == 1 and st["sidecar_fallback_cause"] == "reduced_set", st
             if want == "lite":
                 assert st["sidecar_handbacks"] == 1 and st["sidecar_fell_back"] is False, st
