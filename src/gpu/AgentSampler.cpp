@@ -412,6 +412,7 @@ void Agent::sidecarLoop() {
   const uint64_t tick = 1'000'000;  // 1 ms: the daemon's rate is at most 1 kHz per GPU
   uint64_t next = monoNs();
   uint64_t lastReopenCheck = 0;
+  bool writerGone = false;  // the late heartbeat's writer has exited (its liveness lock is free)
   bool rateWarned = false;
   sidecarGuard_ = BroadcastRateGuard(sidecarReader_->header().sample_hz, kSidecarMinRateFraction, kSidecarRateWindowNs);
   while (!stopFlag_) {
@@ -444,14 +445,20 @@ void Agent::sidecarLoop() {
         if (sidecarFellBack_.load()) return;  // the restarted daemon's sets differ: took over
         continue;
       }
+      writerGone = sidecarReader_->writerGone();
+    } else if (hbAge <= 500'000'000ull) {
+      writerGone = false;
     }
-    // failure detection: a daemon that stopped publishing (killed, hung)
-    // leaves a stale heartbeat; say so once per outage (stats sidecar_stale)
-    const bool stale = hbAge > 3'000'000'000ull;
+    // failure detection: a daemon that stopped publishing leaves a stale
+    // heartbeat; say so once per outage (stats sidecar_stale).  A writer that
+    // is gone (killed, exited) is called stale once its heartbeat is 500 ms
+    // late; a live one that hangs after 3 s.
+    const bool stale = hbAge > 3'000'000'000ull || (writerGone && hbAge > 500'000'000ull);
     if (stale && !sidecarStale_.exchange(true)) {
       sidecarStaleEvents_++;
       LOG(WARNING) << "GPU agent: the daemon's broadcast " << sidecarName_ << " has not been updated for "
-                   << hbAge / 1000000 << " ms (writer pid " << sidecarReader_->header().writer_pid << ")"
+                   << hbAge / 1000000 << " ms (writer pid " << sidecarReader_->header().writer_pid
+                   << (writerGone ? ", exited" : "") << ")"
                    << (fallbackPasses_.empty() ? "; no counter samples until it resumes or restarts"
                                                : "; sampling the GPU in this process from now on");
       // take the GPU's sampling over: the thread continues as samplerLoop

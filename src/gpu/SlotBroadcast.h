@@ -32,14 +32,15 @@
 
 #include <fcntl.h>
 #include <signal.h>
+#include <sys/file.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <cstdint>
-#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -126,6 +127,19 @@ inline std::pair<uint64_t, uint64_t> broadcastSegmentId(const std::string& name)
             : std::pair<uint64_t, uint64_t>{0, 0};
 }
 
+// The writer of the segment open on fd still runs: it holds an exclusive
+// flock on the segment for its whole life (released by the kernel when it
+// exits or is killed), so a shared lock cannot be had.  Unlike kill(pid, 0)
+// this holds across PID namespaces (a daemon on the host, a job in a
+// container).  A writer that predates the lock reads as gone.
+inline bool broadcastWriterHoldsLock(int fd) {
+  if (flock(fd, LOCK_SH | LOCK_NB) == 0) {
+    (void)flock(fd, LOCK_UN);
+    return false;
+  }
+  return errno == EWOULDBLOCK;
+}
+
 // Another process still writes the segment `name`: its writer is alive and
 // its heartbeat younger than maxAgeNs (a writer that hangs, or a dead one
 // whose pid was reused, is replaced).  *who describes it.
@@ -137,6 +151,7 @@ inline bool broadcastWriterActive(const std::string& name, uint64_t maxAgeNs, st
     ::close(fd);
     return false;
   }
+  const bool locked = broadcastWriterHoldsLock(fd);
   void* p = mmap(nullptr, sizeof(SlotBroadcastHeader), PROT_READ, MAP_SHARED, fd, 0);
   ::close(fd);
   if (p == MAP_FAILED) return false;
@@ -146,7 +161,7 @@ inline bool broadcastWriterActive(const std::string& name, uint64_t maxAgeNs, st
   const bool magic = h->magic == kSlotBroadcastMagic;
   munmap(p, sizeof(SlotBroadcastHeader));
   if (!magic || pid == 0 || pid == static_cast<uint32_t>(getpid())) return false;
-  const bool alive = kill(static_cast<pid_t>(pid), 0) == 0 || errno == EPERM;
+  const bool alive = locked || kill(static_cast<pid_t>(pid), 0) == 0 || errno == EPERM;
   const uint64_t now = broadcastMonoNs();
   const bool fresh = hb != 0 && now >= hb && now - hb <= maxAgeNs;
   if (alive && fresh && who) *who = "pid " + std::to_string(pid) + ", heartbeat " + std::to_string((now - hb) / 1000000) + " ms ago";
@@ -195,6 +210,9 @@ class SlotBroadcastWriter {
     struct stat st {};
     (void)fstat(fd, &st);
     (void)fchmod(fd, 0644);  // readable by every local job, whatever the umask
+    // the liveness lock, held until this writer is destroyed or its process
+    // ends (shm_open's descriptor is close-on-exec: no child inherits it)
+    (void)flock(fd, LOCK_EX | LOCK_NB);
     if (ftruncate(fd, static_cast<off_t>(bytes)) != 0) {
       if (err) *err = "ftruncate " + name + ": " + strerror(errno);
       ::close(fd);
@@ -202,13 +220,14 @@ class SlotBroadcastWriter {
       return nullptr;
     }
     void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    ::close(fd);
     if (p == MAP_FAILED) {
       if (err) *err = "mmap " + name + ": " + strerror(errno);
+      ::close(fd);
       shm_unlink(name.c_str());
       return nullptr;
     }
     auto w = std::unique_ptr<SlotBroadcastWriter>(new SlotBroadcastWriter());
+    w->lockFd_ = fd;
     w->name_ = name;
     w->bytes_ = bytes;
     w->dev_ = static_cast<uint64_t>(st.st_dev);
@@ -243,6 +262,7 @@ class SlotBroadcastWriter {
     // keeps its name
     if (!name_.empty() && broadcastSegmentId(name_) == std::pair<uint64_t, uint64_t>{dev_, ino_})
       shm_unlink(name_.c_str());
+    if (lockFd_ >= 0) ::close(lockFd_);  // readers see this writer gone from here on
   }
   // raw (with meta) only when the segment carries raw samples; R <= raw_stride
   void publish(const DynoSlot& s, const DynoStepMeta* meta = nullptr, const double* raw = nullptr, size_t R = 0) {
@@ -276,6 +296,7 @@ class SlotBroadcastWriter {
   std::string name_;
   size_t bytes_ = 0;
   uint64_t dev_ = 0, ino_ = 0;  // the segment this writer created
+  int lockFd_ = -1;             // holds the liveness lock
   SlotBroadcastHeader* hdr_ = nullptr;
   DynoSlot* slots_ = nullptr;
   uint8_t* raw_ = nullptr;
@@ -297,9 +318,9 @@ class SlotBroadcastReader {
     }
     const size_t bytes = static_cast<size_t>(st.st_size);
     void* p = mmap(nullptr, bytes, PROT_READ, MAP_SHARED, fd, 0);
-    ::close(fd);
     if (p == MAP_FAILED) {
       if (err) *err = "mmap " + name + ": " + strerror(errno);
+      ::close(fd);
       return nullptr;
     }
     auto* h = static_cast<const SlotBroadcastHeader*>(p);
@@ -315,9 +336,11 @@ class SlotBroadcastReader {
         sizeof(SlotBroadcastHeader) + h->capacity * sizeof(DynoSlot) > bytes || rawBad) {
       if (err) *err = "slot broadcast " + name + " has a bad header";
       munmap(p, bytes);
+      ::close(fd);
       return nullptr;
     }
     auto r = std::unique_ptr<SlotBroadcastReader>(new SlotBroadcastReader());
+    r->fd_ = fd;  // kept: the writer's liveness lock is tested through it
     r->bytes_ = bytes;
     r->hdr_ = h;
     r->name_ = name;
@@ -332,7 +355,12 @@ class SlotBroadcastReader {
   }
   ~SlotBroadcastReader() {
     if (hdr_) munmap(const_cast<SlotBroadcastHeader*>(hdr_), bytes_);
+    if (fd_ >= 0) ::close(fd_);
   }
+  // The writer of this segment has exited or was killed (its liveness lock is
+  // free): a late heartbeat will not come back.  Also true for a writer that
+  // predates the lock, so callers ask only once the heartbeat is late.
+  bool writerGone() const { return fd_ >= 0 && !broadcastWriterHoldsLock(fd_); }
   // Up to `max` slots from the cursor on, oldest first, into out; returns how
   // many.  *lost grows by the slots overwritten before they could be read.
   size_t read(DynoSlot* out, size_t max, uint64_t* lost) {
@@ -429,6 +457,7 @@ class SlotBroadcastReader {
   size_t bytes_ = 0;
   std::string name_;
   std::pair<uint64_t, uint64_t> id_{0, 0};  // (st_dev, st_ino) of the mapped segment
+  int fd_ = -1;
   const SlotBroadcastHeader* hdr_ = nullptr;
   const DynoSlot* slots_ = nullptr;
   const uint8_t* raw_ = nullptr;

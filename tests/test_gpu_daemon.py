@@ -603,7 +603,10 @@ def test_sidecar_reports_a_dead_daemon(native_built):
     (SIGKILL, its broadcast segment left behind with a frozen heartbeat) while
     a job's agent reads it.  The job keeps training; the agent flags the
     outage (sidecar_stale, one event, a warning) and takes the GPU's sampling
-    over in process: its own samples keep arriving at ~1 kHz."""
+    over in process: its own samples keep arriving at ~1 kHz.  The killed
+    writer's liveness lock is free, so the outage is called after 500 ms of
+    silence, not the 3 s a live but hung writer gets: the 2 s ending 3.5 s
+    after the kill are all the job's own samples."""
     flag = os.path.join(tempfile.mkdtemp(prefix="dyside"), "done")
     d = DaemonProcess(["--enable_gpu_counters", "--gpu_counter_hz=1000", "--gpu_counters=lite"]).start()
     try:
@@ -618,17 +621,17 @@ def test_sidecar_reports_a_dead_daemon(native_built):
             time.sleep(1.0)
             d.proc.kill()  # no clean shutdown: the segment stays, its heartbeat stops
             d.proc.wait(timeout=30)
-            time.sleep(7.0)  # 3 s to call it stale, then in-process sampling
+            time.sleep(3.5)  # ~0.75 s to call it stale, then in-process sampling
             rc = c.finish(flag, timeout=60)
             res = [json.loads(l[7:]) for l in c.lines("RESULT ")]
             assert rc == 0 and res, c.tails()
             st = res[0]
             assert st["sampler"] == "daemon" and st["samples_taken"] > 500, st
             assert st["sidecar_stale"] is True and st["sidecar_stale_events"] == 1, st
-            assert "has not been updated" in c.stderr(), c.tails()
+            assert "has not been updated" in c.stderr() and ", exited)" in c.stderr(), c.tails()
             assert st["sidecar_fell_back"] is True and st["sidecar_fallback_after_ms"] > 0, st
             assert st["sidecar_fallback_cause"] == "daemon_stale", st
-            assert st["last_2s"] > 1500, st  # the job's own 1 kHz after the fallback
+            assert st["last_2s"] > 1900, st  # the job's own 1 kHz since well before the window
             assert st["samples_failed"] == 0 and st["last_error"] == "", st
     finally:
         d.stop()

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6 g07: the sidecar hand-back (a job that took its GPU's sampling over
+# round 6 g07/g08: the sidecar hand-back (a job that took its GPU's sampling over
 # returns to a healthy daemon) and every other sidecar test
 set -o pipefail
 O=gpurun_out/r6g07; mkdir -p $O
