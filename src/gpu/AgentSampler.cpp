@@ -411,7 +411,7 @@ void Agent::sidecarLoop() {
   bool wasPaused = false;
   const uint64_t tick = 1'000'000;  // 1 ms: the daemon's rate is at most 1 kHz per GPU
   uint64_t next = monoNs();
-  uint64_t lastReopenCheck = 0;
+  uint64_t lastReopenCheck = 0, lastGoneCheck = 0;
   bool writerGone = false;  // the late heartbeat's writer has exited (its liveness lock is free)
   bool rateWarned = false;
   sidecarGuard_ = BroadcastRateGuard(sidecarReader_->header().sample_hz, kSidecarMinRateFraction, kSidecarRateWindowNs);
@@ -445,15 +445,20 @@ void Agent::sidecarLoop() {
         if (sidecarFellBack_.load()) return;  // the restarted daemon's sets differ: took over
         continue;
       }
-      writerGone = sidecarReader_->writerGone();
-    } else if (hbAge <= 500'000'000ull) {
+    }
+    // a heartbeat 50 ms late (the daemon beats every sample, every 2 ms when
+    // paused): is its writer still there?  (one flock call per 50 ms)
+    if (hbAge <= 50'000'000ull) {
       writerGone = false;
+    } else if (now - lastGoneCheck >= 50'000'000ull) {
+      lastGoneCheck = now;
+      writerGone = sidecarReader_->writerGone();
     }
     // failure detection: a daemon that stopped publishing leaves a stale
     // heartbeat; say so once per outage (stats sidecar_stale).  A writer that
-    // is gone (killed, exited) is called stale once its heartbeat is 500 ms
-    // late; a live one that hangs after 3 s.
-    const bool stale = hbAge > 3'000'000'000ull || (writerGone && hbAge > 500'000'000ull);
+    // is gone (killed, exited) is called stale at once (its heartbeat 50 ms
+    // late); a live one that hangs after 3 s.
+    const bool stale = hbAge > 3'000'000'000ull || writerGone;
     if (stale && !sidecarStale_.exchange(true)) {
       sidecarStaleEvents_++;
       LOG(WARNING) << "GPU agent: the daemon's broadcast " << sidecarName_ << " has not been updated for "
@@ -710,6 +715,7 @@ bool Agent::sidecarFallback(const char* why, int cause) {
   sidecarFallbackCause_ = cause;
   sidecarTakeovers_++;
   handBackGate_.reset();
+  handBackGate_.setTarget(sidecarReader_->header().sample_hz, kSidecarMinRateFraction);
   sidecarFellBack_ = true;
   LOG(WARNING) << "GPU agent: " << why << "; this process now samples " << pciLocString(pciLoc_)
                << " itself (" << passes_[0].R << " counter instances)";
@@ -719,8 +725,8 @@ bool Agent::sidecarFallback(const char* why, int cause) {
 // After a takeover (samplerLoop, every 500 ms): is the daemon healthy again?
 // Its broadcast -- or a restarted daemon's new segment with the same layouts,
 // which the pass table's daemon entries still describe -- must be live
-// (heartbeat < 200 ms, not paused), on its full set and at >= 98 % of its
-// rate over its last second, at every check for the gate's hold.  Then this
+// (heartbeat < 200 ms, not paused) and on its full set at every check for the
+// gate's hold, and have published >= 98 % of its rate over the hold.  Then this
 // process stops its own context and returns to staging the daemon's samples;
 // the passes go back to fallbackPasses_ with their layouts and pass-table
 // entries, so a later takeover only restarts pass 0.  A daemon that stays
@@ -730,7 +736,7 @@ bool Agent::sidecarHandBack(uint64_t now) {
     std::string e;
     auto r = SlotBroadcastReader::open(sidecarName_, &e);
     if (!r || !r->carriesRaw() || !r->sameLayouts(*sidecarReader_) || !r->live(now, 200'000'000ull)) {
-      handBackGate_.observe(now, false);
+      handBackGate_.observe(now, false, 0);
       return false;
     }
     std::lock_guard<std::mutex> g(sidecarMu_);
@@ -738,10 +744,8 @@ bool Agent::sidecarHandBack(uint64_t now) {
     sidecarReattaches_++;
   }
   const auto& h = sidecarReader_->header();
-  const uint64_t mhz = h.rate_mhz.load(std::memory_order_relaxed);
-  const bool healthy = sidecarReader_->live(now, 200'000'000ull) && h.full_set.load(std::memory_order_relaxed) != 0 &&
-                       mhz != 0 && static_cast<double>(mhz) >= 1000.0 * kSidecarMinRateFraction * h.sample_hz;
-  if (!handBackGate_.observe(now, healthy)) return false;
+  const bool healthy = sidecarReader_->live(now, 200'000'000ull) && h.full_set.load(std::memory_order_relaxed) != 0;
+  if (!handBackGate_.observe(now, healthy, sidecarReader_->head())) return false;
   sampler_->stop();
   {
     std::lock_guard<std::mutex> g(passesMu_);
@@ -759,7 +763,7 @@ bool Agent::sidecarHandBack(uint64_t now) {
   sidecarHandBackHoldNs_ = handBackGate_.holdNs();
   sidecarFellBack_ = false;
   LOG(WARNING) << "GPU agent: the daemon's broadcast " << sidecarName_ << " is healthy again (writer pid "
-               << h.writer_pid << ", " << mhz * 1e-3 << " samples/s); sampling through it again";
+               << h.writer_pid << ", " << handBackGate_.lastRateHz() << " samples/s over the hold); sampling through it again";
   return true;
 }
 

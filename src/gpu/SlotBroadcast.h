@@ -473,35 +473,55 @@ class SlotBroadcastReader {
 // serialising inside one daemon would otherwise cost the job its rate
 // silently: the heartbeat stays fresh).
 // When may a job that took its GPU's sampling over hand it back to the
-// daemon?  Once the broadcast has looked healthy (live, on its full set, at
-// its rate) at every check for holdNs; each hand-back doubles the hold for
-// the next one (up to maxHoldNs), so a daemon that keeps failing costs the
-// job a few switches, not a flapping sampler.
+// daemon?  Once the broadcast has been live and on its full set at every
+// check for holdNs, and has published at least minFraction x hz over that
+// whole hold (the average: a daemon reading beside the job's own context
+// has its slow seconds, which a per-second bar would hold against it
+// forever).  Each hand-back doubles the hold for the next one (up to
+// maxHoldNs), so a daemon that keeps failing costs the job a few switches,
+// not a flapping sampler.
 class HandBackGate {
  public:
-  explicit HandBackGate(uint64_t holdNs = 3'000'000'000ull, uint64_t maxHoldNs = 120'000'000'000ull)
-      : hold_(holdNs), maxHold_(maxHoldNs) {}
+  explicit HandBackGate(double hz = 1000.0, double minFraction = 0.98, uint64_t holdNs = 3'000'000'000ull,
+                        uint64_t maxHoldNs = 120'000'000'000ull)
+      : hz_(hz), minFraction_(minFraction), hold_(holdNs), maxHold_(maxHoldNs) {}
   void reset() { since_ = 0; }  // a takeover: the hold starts over
-  // true when the broadcast has been healthy for the whole hold: hand back now
-  bool observe(uint64_t nowNs, bool healthy) {
-    if (!healthy || nowNs < since_) {
+  void setTarget(double hz, double minFraction) {
+    hz_ = hz;
+    minFraction_ = minFraction;
+  }
+  // true when the broadcast has been healthy for the whole hold: hand back
+  // now.  head: the broadcast's published count.
+  bool observe(uint64_t nowNs, bool healthy, uint64_t head) {
+    if (!healthy || nowNs < since_ || (since_ != 0 && head < head0_)) {
       since_ = 0;
       return false;
     }
     if (since_ == 0) {
       since_ = nowNs;
+      head0_ = head;
       return false;
     }
     if (nowNs - since_ < hold_) return false;
+    const double rate = static_cast<double>(head - head0_) * 1e9 / static_cast<double>(nowNs - since_);
+    lastRateHz_ = rate;
+    if (rate < minFraction_ * hz_) {  // short over the hold: a new hold from here
+      since_ = nowNs;
+      head0_ = head;
+      return false;
+    }
     since_ = 0;
     hold_ = std::min(hold_ * 2, maxHold_);
     return true;
   }
   uint64_t holdNs() const { return hold_; }  // the next hand-back's
+  double lastRateHz() const { return lastRateHz_; }  // over the last completed hold
 
  private:
+  double hz_, minFraction_;
   uint64_t hold_, maxHold_;
-  uint64_t since_ = 0;
+  uint64_t since_ = 0, head0_ = 0;
+  double lastRateHz_ = 0.0;
 };
 
 class BroadcastRateGuard {

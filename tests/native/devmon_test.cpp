@@ -515,32 +515,40 @@ TEST(DevMon, RateGuardWindows) {
 }
 
 // The hand-back gate: a job that took over returns to the daemon only after
-// the broadcast has been healthy at every check for the hold; one unhealthy
-// check restarts it; each hand-back doubles the next hold, up to the cap.
+// the broadcast has been live and on its full set at every check for the
+// hold, and published >= 98 % of its rate over the whole hold (an average:
+// one slow second inside it is fine); one unhealthy check restarts the hold;
+// each hand-back doubles the next, up to the cap.
 TEST(DevMon, HandBackGateHoldsAndBacksOff) {
   const uint64_t s = 1'000'000'000ull;
-  HandBackGate g(3 * s, 10 * s);
-  uint64_t t = 100 * s;
-  EXPECT_FALSE(g.observe(t, true));  // the hold starts
-  EXPECT_FALSE(g.observe(t + 2 * s, true));
-  EXPECT_FALSE(g.observe(t + 2 * s + s / 2, false));  // unhealthy: starts over
-  EXPECT_FALSE(g.observe(t + 3 * s, true));
-  EXPECT_FALSE(g.observe(t + 5 * s, true));
-  EXPECT_TRUE(g.observe(t + 6 * s, true));  // 3 s healthy
+  HandBackGate g(1000.0, 0.98, 3 * s, 10 * s);
+  uint64_t t = 100 * s, h = 5000;
+  EXPECT_FALSE(g.observe(t, true, h));  // the hold starts
+  EXPECT_FALSE(g.observe(t + 2 * s, true, h + 2000));
+  EXPECT_FALSE(g.observe(t + 2 * s + s / 2, false, h + 2500));  // unhealthy: starts over
+  EXPECT_FALSE(g.observe(t + 3 * s, true, h + 3000));
+  EXPECT_FALSE(g.observe(t + 4 * s, true, h + 3900));  // a slow second (900 samples)...
+  EXPECT_TRUE(g.observe(t + 6 * s, true, h + 5960));   // ...but 2960 over the 3 s hold
+  EXPECT_NEAR(g.lastRateHz(), 986.7, 0.1);
   EXPECT_EQ(g.holdNs(), 6 * s);
-  t += 20 * s;
+  // short over a whole hold: a new hold from there
+  t += 20 * s, h += 20000;
   g.reset();  // the next takeover
-  EXPECT_FALSE(g.observe(t, true));
-  EXPECT_FALSE(g.observe(t + 5 * s, true));
-  EXPECT_TRUE(g.observe(t + 6 * s, true));
-  EXPECT_EQ(g.holdNs(), 10 * s);  // capped
-  t += 20 * s;
-  EXPECT_FALSE(g.observe(t, true));
-  EXPECT_FALSE(g.observe(t + 9 * s, true));
-  EXPECT_TRUE(g.observe(t + 10 * s, true));
+  EXPECT_FALSE(g.observe(t, true, h));
+  EXPECT_FALSE(g.observe(t + 6 * s, true, h + 5000));  // 833/s
+  EXPECT_FALSE(g.observe(t + 11 * s, true, h + 10000));
+  EXPECT_TRUE(g.observe(t + 12 * s, true, h + 11000));  // 6 s at 1000/s since t + 6 s
+  EXPECT_EQ(g.holdNs(), 10 * s);                        // capped
+  t += 20 * s, h += 20000;
+  EXPECT_FALSE(g.observe(t, true, h));
+  EXPECT_FALSE(g.observe(t + 9 * s, true, h + 9000));
+  EXPECT_TRUE(g.observe(t + 10 * s, true, h + 10000));
   EXPECT_EQ(g.holdNs(), 10 * s);
-  // a clock that goes backwards (a reset timestamp) never hands back early
-  EXPECT_FALSE(g.observe(t + 30 * s, true));
-  EXPECT_FALSE(g.observe(t + 29 * s, true));
-  EXPECT_FALSE(g.observe(t + 30 * s, true));
+  // a restarted writer (its count starts over) or a clock that goes
+  // backwards never hands back early
+  EXPECT_FALSE(g.observe(t + 30 * s, true, h + 30000));
+  EXPECT_FALSE(g.observe(t + 35 * s, true, 100));
+  EXPECT_FALSE(g.observe(t + 36 * s, true, 1100));
+  EXPECT_FALSE(g.observe(t + 35 * s, true, 1200));
+  EXPECT_FALSE(g.observe(t + 36 * s, true, 2200));
 }
