@@ -276,10 +276,10 @@ class Agent {
   uint64_t stepCompleted();          // newest completed launch's end (packMu_)
   std::atomic<uint64_t> stepLaunches_{0}, stagePacked_{0}, stageFull_{0};
   // sampler "daemon" (the sidecar)
-  bool sidecar_ = false;
+  std::atomic<bool> sidecar_{false};  // the sidecar machinery is on (from start, or a late join)
   std::unique_ptr<SlotBroadcastReader> sidecarReader_;
   std::string sidecarName_;
-  uint64_t sidecarPciLoc_ = 0;  // pci_loc in the broadcast's header
+  std::atomic<uint64_t> sidecarPciLoc_{0};  // pci_loc in the broadcast's header
   // raw sidecar: the daemon's counter layouts as step-kernel passes
   bool sidecarRaw_ = false;
   struct SidecarLayout {
@@ -300,7 +300,7 @@ class Agent {
   std::vector<PassState> retiredPasses_;  // a failed second takeover's: layouts freed at stop
   int agentIdx_ = -1;
   uint32_t passIdxBase_ = 0;
-  int stepPassCount_ = 1;                          // entries of dStepPasses_
+  std::atomic<int> stepPassCount_{1};              // entries of dStepPasses_ in use
   std::atomic<bool> sidecarFellBack_{false};
   std::atomic<uint64_t> sidecarFallbackNs_{0};
   mutable std::mutex passesMu_;                    // passes_ against stats() while it changes
@@ -310,6 +310,19 @@ class Agent {
   // its full set and at 98 % of its rate for HandBackGate's hold; the passes
   // return to fallbackPasses_ with their layouts, for the next takeover.
   bool sidecarHandBack(uint64_t now);              // sampler thread (in samplerLoop)
+  // Late join (sampler "auto" that started in process, e.g. before the node's
+  // daemon): once a broadcast for this GPU is live with this job's set and
+  // rate for the gate's hold, its layouts get pass-table entries after this
+  // process's own passes (sidecarIdxBase_) and the thread continues as the
+  // sidecar, its own passes armed as the fallback (fallbackIdxBase_ 0).
+  bool sidecarJoin(uint64_t now);                  // sampler thread (in samplerLoop)
+  bool autoJoin_ = false;                          // this start may join a daemon later
+  std::unique_ptr<SlotBroadcastReader> joinReader_;  // sampler thread: the candidate
+  HandBackGate joinGate_;                          // sampler thread
+  std::atomic<uint64_t> sidecarJoins_{0};
+  uint32_t sidecarIdxBase_ = 0;    // pass-table index of the daemon's layout 0
+  uint32_t fallbackIdxBase_ = 0;   // ... and of this process's own pass 0 when it samples
+  uint32_t stepPassCap_ = 0;       // entries allocated in dStepPasses_
   HandBackGate handBackGate_;                      // sampler thread
   std::atomic<uint64_t> sidecarTakeovers_{0}, sidecarHandBacks_{0};
   std::atomic<uint64_t> sidecarHandBackHoldNs_{0};
