@@ -494,7 +494,9 @@ class GpuAgent:
         daemon's, same sets) has been live, on its full set and at 98 % of its
         rate for 3 s (doubling with each hand-back), this process stops its
         own context and samples through the daemon again (stats
-        ``sidecar_takeovers``, ``sidecar_handbacks``).  With sampler "auto" the daemon
+        ``sidecar_takeovers``, ``sidecar_handbacks``); with sampler "auto" a
+        job that started in process likewise joins a daemon that comes up
+        later, at its set and rate (``sidecar_joins``).  With sampler "auto" the daemon
         is taken only when its broadcast is live, on the full set, at this
         job's ``sample_hz`` and ``counter_set`` (stats ``sampler_auto_reason``)."""
         if not _preinit_done:
