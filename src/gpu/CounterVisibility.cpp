@@ -182,7 +182,8 @@ ProcScanCache::Entry& ProcScanCache::entry(int pid, uint64_t nowNs) {
     for (auto it = by_.begin(); it != by_.end();) {
       const bool stale = nowNs - it->second.localNs > 10 * ttlNs_ &&
                          std::all_of(it->second.countable.begin(), it->second.countable.end(),
-                                     [&](const auto& kv) { return nowNs - kv.second.first > 10 * ttlNs_; });
+                                     [&](const auto& kv) { return nowNs - kv.second.first > 10 * ttlNs_; }) &&
+                         !departing(it->first, nowNs);
       it = stale ? by_.erase(it) : std::next(it);
     }
     lastPruneNs_ = nowNs;
@@ -190,6 +191,10 @@ ProcScanCache::Entry& ProcScanCache::entry(int pid, uint64_t nowNs) {
   const uint64_t st = procStartTime(procRoot_, pid);
   ++reads_;
   Entry& e = by_[pid];
+  if (st == 0 && e.startTime != 0) {  // the process is gone from /proc: keep what was known
+    if (e.vramNs != 0 && e.departNs == 0) e.departNs = nowNs;
+    return e;
+  }
   if (e.startTime != st) {  // a new process behind this pid (or a new entry)
     e = Entry{};
     e.startTime = st;
@@ -200,12 +205,30 @@ ProcScanCache::Entry& ProcScanCache::entry(int pid, uint64_t nowNs) {
 const LocalGpuProcess& ProcScanCache::local(int pid, uint64_t nowNs) {
   Entry& e = entry(pid, nowNs);
   if (!e.haveLocal || nowNs - e.localNs > ttlNs_) {
-    e.lp = localGpuProcess(pid, procRoot_);
+    LocalGpuProcess lp = localGpuProcess(pid, procRoot_);
+    if (!lp.vramKiB.empty()) {
+      e.vramNs = nowNs;
+      e.departNs = 0;
+      e.lp = std::move(lp);
+    } else if (e.vramNs != 0) {
+      // held GPU memory, holds none now (exiting: its fds are closing): keep
+      // the last view while it departs, the current one after the grace
+      if (e.departNs == 0) e.departNs = nowNs;
+      else if (nowNs - e.departNs > kDepartingGraceNs) e.lp = std::move(lp);
+    } else {
+      e.lp = std::move(lp);
+    }
     e.localNs = nowNs;
     e.haveLocal = true;
     ++reads_;
   }
   return e.lp;
+}
+
+bool ProcScanCache::departing(int pid, uint64_t nowNs) const {
+  const auto it = by_.find(pid);
+  return it != by_.end() && it->second.vramNs != 0 && it->second.departNs != 0 &&
+         nowNs - it->second.departNs <= kDepartingGraceNs;
 }
 
 bool ProcScanCache::countable(int pid, uint64_t gpuId, uint64_t nowNs) {
@@ -236,16 +259,18 @@ namespace {
 constexpr uint64_t kMinStandInVramKiB = 512;
 
 // the visibility logic, over how a process's /proc state is obtained
-template <typename LocalFn, typename CountableFn, typename AllFn>
+template <typename LocalFn, typename CountableFn, typename AllFn, typename DepartingFn>
 GpuVisibility visibilityOf(uint64_t gpuId, const std::string& bdf, int selfPid, const std::vector<KfdProcess>& procs,
-                           LocalFn&& localOf, CountableFn&& countableOf, AllFn&& localsFn) {
+                           LocalFn&& localOf, CountableFn&& countableOf, AllFn&& localsFn, DepartingFn&& departingOf) {
   GpuVisibility v;
   v.known = true;
   std::set<int> seen;
   int rest = 0;  // KFD processes not numbered as in this namespace
   for (const auto& kp : procs) {
     if (!kp.gpus.count(gpuId)) continue;
-    if (localOf(kp.pid).vramKiB.count(bdf)) {
+    const LocalGpuProcess& lp = localOf(kp.pid);
+    if (departingOf(kp.pid)) continue;  // exiting: KFD still lists it
+    if (lp.vramKiB.count(bdf)) {
       if (kp.pid == selfPid) continue;
       seen.insert(kp.pid);
       v.pids.push_back(kp.pid);
@@ -279,7 +304,8 @@ GpuVisibility gpuVisibility(uint64_t gpuId, const std::string& bdf, int selfPid,
   return visibilityOf(
       gpuId, bdf, selfPid, procs, [&](int pid) -> const LocalGpuProcess& { return cache.local(pid, nowNs); },
       [&](int pid) { return cache.countable(pid, gpuId, nowNs); },
-      [&]() -> const std::vector<LocalGpuProcess>& { return cache.all(nowNs); });
+      [&]() -> const std::vector<LocalGpuProcess>& { return cache.all(nowNs); },
+      [&](int pid) { return cache.departing(pid, nowNs); });
 }
 
 GpuVisibility gpuVisibility(uint64_t gpuId, const std::string& bdf, int selfPid, const std::vector<KfdProcess>& procs,
@@ -292,7 +318,7 @@ GpuVisibility gpuVisibility(uint64_t gpuId, const std::string& bdf, int selfPid,
         lp = localGpuProcess(pid, procRoot);
         return lp;
       },
-      [&](int pid) { return processCountable(pid, gpuId, procRoot); }, localsFn);
+      [&](int pid) { return processCountable(pid, gpuId, procRoot); }, localsFn, [](int) { return false; });
 }
 
 GpuVisibility gpuVisibility(uint64_t gpuId, const std::string& bdf, int selfPid, const std::string& kfdRoot,

@@ -118,12 +118,22 @@ class ProcScanCache {
   const LocalGpuProcess& local(int pid, uint64_t nowNs);
   bool countable(int pid, uint64_t gpuId, uint64_t nowNs);
   const std::vector<LocalGpuProcess>& all(uint64_t nowNs);  // the full scan, same ttl
+  // A process seen holding GPU memory here that is now leaving: its /proc
+  // entry is gone, or it holds no GPU memory any more, for at most
+  // kDepartingGraceNs.  KFD lists a process until its (asynchronous) teardown
+  // has finished, after its fds and even its /proc entry are gone: without
+  // this a job that exits looks like another namespace's process for that
+  // long, and an auto-set daemon drops to its readable-only set for nothing.
+  bool departing(int pid, uint64_t nowNs) const;
+  static constexpr uint64_t kDepartingGraceNs = 30'000'000'000ull;
   const std::string& procRoot() const { return procRoot_; }
   uint64_t reads() const { return reads_; }                  // /proc reads done (tests)
 
  private:
   struct Entry {
     uint64_t startTime = 0, localNs = 0;
+    uint64_t vramNs = 0;    // last seen holding GPU memory
+    uint64_t departNs = 0;  // since then: gone from /proc, or no GPU memory
     bool haveLocal = false;
     LocalGpuProcess lp;
     std::map<uint64_t, std::pair<uint64_t, bool>> countable;  // gpu -> (time, result)

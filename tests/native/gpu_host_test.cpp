@@ -1323,3 +1323,39 @@ TEST(GpuHost, SlotBroadcastCarriesRawSamples) {
   EXPECT_TRUE(!r2->carriesRaw());
   EXPECT_EQ(r2->layoutCount(), 0u);
 }
+
+// A job that exits: KFD keeps listing it until its teardown has finished,
+// after its fds and even its /proc entry are gone.  The cache remembers it
+// held GPU memory here and treats it as departing (neither another
+// namespace's process nor uncountable) for the grace period, so an auto-set
+// daemon does not drop to its readable-only set for nothing.
+TEST(GpuHost, ExitingJobIsDepartingNotForeign) {
+  FakeTree t;
+  t.kfdProc(100, 12345);
+  t.kfdProc(200, 12345);
+  t.proc(100, kBdfA, 1000, "7f40-7f41 r--s 0 00:01 9 /memfd:dynolog-countable:12345 (deleted)\n");
+  t.proc(200, kBdfA, 1000, "7f40-7f41 r--s 0 00:01 9 /memfd:dynolog-countable:12345 (deleted)\n");
+  t.put("proc/100/stat", "100 (python) S 1 100 100 0 -1 0 0 0 0 0 0 0 0 0 20 0 1 0 5000 0 0\n");
+  t.put("proc/200/stat", "200 (python) S 1 200 200 0 -1 0 0 0 0 0 0 0 0 0 20 0 1 0 6000 0 0\n");
+  const uint64_t s = 1'000'000'000ull;
+  ProcScanCache cache(t.root + "/proc", 1 * s);
+  auto procs = kfdProcesses(t.root + "/kfd");
+  EXPECT_TRUE(gpuVisibility(12345, kBdfA, 400, procs, cache, 10 * s).full());
+  // 100 exits: its /proc entry goes, KFD still lists it
+  ASSERT_EQ(system(("rm -rf " + t.root + "/proc/100").c_str()), 0);
+  // 200 is exiting: fds closed (no GPU memory), /proc entry still there
+  ASSERT_EQ(system(("rm -rf " + t.root + "/proc/200/fd " + t.root + "/proc/200/fdinfo").c_str()), 0);
+  auto v = gpuVisibility(12345, kBdfA, 400, procs, cache, 12 * s);
+  EXPECT_TRUE(v.full());
+  EXPECT_EQ(v.foreign, 0);
+  EXPECT_TRUE(cache.departing(100, 12 * s));
+  EXPECT_TRUE(cache.departing(200, 12 * s));
+  EXPECT_TRUE(gpuVisibility(12345, kBdfA, 400, procs, cache, 30 * s).full());
+  // still listed long after the grace: counted as KFD processes not resolvable here
+  v = gpuVisibility(12345, kBdfA, 400, procs, cache, 12 * s + ProcScanCache::kDepartingGraceNs + 2 * s);
+  v = gpuVisibility(12345, kBdfA, 400, procs, cache, 12 * s + ProcScanCache::kDepartingGraceNs + 4 * s);
+  EXPECT_FALSE(v.full());
+  EXPECT_EQ(v.foreign, 2);
+  // the uncached check has no history: an exited job there is another namespace's
+  EXPECT_FALSE(gpuVisibility(12345, kBdfA, 400, t.root + "/kfd", t.root + "/proc").full());
+}
