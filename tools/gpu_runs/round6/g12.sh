@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 6 g12: an exiting job is 'departing' for the daemon's visibility (g11
+# saw the daemon drop to its readable-only set as a countable job exited);
+# the daemon test file and the native suite at the box's strict rates
+set -o pipefail
+O=gpurun_out/r6g12; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -v --timeout 240 --timeout-method thread -s \
+  tests/test_gpu_daemon.py tests/test_native.py -m gpu > $O/pytest.log 2>&1; rc=$?
+grep -E "PASSED|FAILED|passed|failed" $O/pytest.log | tail -40
+exit $rc
