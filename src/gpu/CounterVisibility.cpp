@@ -161,6 +161,12 @@ std::vector<LocalGpuProcess> localGpuProcesses(const std::string& procRoot) {
 }
 
 namespace {
+// A stand-in must hold real memory on the GPU: a process that only brought
+// the runtime up (the torchrun launcher holds 44 KiB on GPU 0 after torch
+// counted the devices, profiles/round5/g21) has launched nothing.  Any kernel
+// launch loads code objects and kernel arguments into VRAM, far above this.
+constexpr uint64_t kMinStandInVramKiB = 512;
+
 // /proc/<pid>/stat field 22 (start time in clock ticks): tells a reused pid
 uint64_t procStartTime(const std::string& procRoot, int pid) {
   std::ifstream f(procRoot + "/" + std::to_string(pid) + "/stat");
@@ -247,21 +253,40 @@ const std::vector<LocalGpuProcess>& ProcScanCache::all(uint64_t nowNs) {
     allNs_ = nowNs;
     haveAll_ = true;
     ++reads_;
+    for (const auto& lp : all_) {
+      for (const auto& kv : lp.vramKiB) {
+        if (kv.second < kMinStandInVramKiB || !lp.kfd) continue;  // as for a stand-in
+        auto& h = heldVram_[lp.pid];
+        h.first = nowNs;
+        h.second.insert(kv.first);
+      }
+    }
+    for (auto it = heldVram_.begin(); it != heldVram_.end();)
+      it = nowNs - it->second.first > kDepartingGraceNs ? heldVram_.erase(it) : std::next(it);
   }
   return all_;
 }
 
+int ProcScanCache::departingStandIns(const std::string& bdf, uint64_t nowNs) const {
+  int n = 0;
+  for (const auto& [pid, h] : heldVram_) {
+    if (nowNs - h.first > kDepartingGraceNs || !h.second.count(bdf)) continue;
+    const bool holdsNow = std::any_of(all_.begin(), all_.end(), [&, p = pid](const LocalGpuProcess& lp) {
+      const auto vr = lp.vramKiB.find(bdf);
+      return lp.pid == p && lp.kfd && vr != lp.vramKiB.end() && vr->second >= kMinStandInVramKiB;
+    });
+    if (!holdsNow) ++n;
+  }
+  return n;
+}
+
 namespace {
-// A stand-in must hold real memory on the GPU: a process that only brought
-// the runtime up (the torchrun launcher holds 44 KiB on GPU 0 after torch
-// counted the devices, profiles/round5/g21) has launched nothing.  Any kernel
-// launch loads code objects and kernel arguments into VRAM, far above this.
-constexpr uint64_t kMinStandInVramKiB = 512;
 
 // the visibility logic, over how a process's /proc state is obtained
-template <typename LocalFn, typename CountableFn, typename AllFn, typename DepartingFn>
+template <typename LocalFn, typename CountableFn, typename AllFn, typename DepartingFn, typename LeftFn>
 GpuVisibility visibilityOf(uint64_t gpuId, const std::string& bdf, int selfPid, const std::vector<KfdProcess>& procs,
-                           LocalFn&& localOf, CountableFn&& countableOf, AllFn&& localsFn, DepartingFn&& departingOf) {
+                           LocalFn&& localOf, CountableFn&& countableOf, AllFn&& localsFn, DepartingFn&& departingOf,
+                           LeftFn&& departedStandIns) {
   GpuVisibility v;
   v.known = true;
   std::set<int> seen;
@@ -294,7 +319,7 @@ GpuVisibility visibilityOf(uint64_t gpuId, const std::string& bdf, int selfPid, 
     v.pids.push_back(lp.pid);
     if (!countableOf(lp.pid)) v.uncountable.push_back(lp.pid);
   }
-  v.foreign = std::max(0, rest - standIns - (selfHere ? 1 : 0));
+  v.foreign = std::max(0, rest - standIns - (selfHere ? 1 : 0) - departedStandIns());
   return v;
 }
 }  // namespace
@@ -305,7 +330,8 @@ GpuVisibility gpuVisibility(uint64_t gpuId, const std::string& bdf, int selfPid,
       gpuId, bdf, selfPid, procs, [&](int pid) -> const LocalGpuProcess& { return cache.local(pid, nowNs); },
       [&](int pid) { return cache.countable(pid, gpuId, nowNs); },
       [&]() -> const std::vector<LocalGpuProcess>& { return cache.all(nowNs); },
-      [&](int pid) { return cache.departing(pid, nowNs); });
+      [&](int pid) { return cache.departing(pid, nowNs); },
+      [&]() { return cache.departingStandIns(bdf, nowNs); });
 }
 
 GpuVisibility gpuVisibility(uint64_t gpuId, const std::string& bdf, int selfPid, const std::vector<KfdProcess>& procs,
@@ -318,7 +344,8 @@ GpuVisibility gpuVisibility(uint64_t gpuId, const std::string& bdf, int selfPid,
         lp = localGpuProcess(pid, procRoot);
         return lp;
       },
-      [&](int pid) { return processCountable(pid, gpuId, procRoot); }, localsFn, [](int) { return false; });
+      [&](int pid) { return processCountable(pid, gpuId, procRoot); }, localsFn, [](int) { return false; },
+      []() { return 0; });
 }
 
 GpuVisibility gpuVisibility(uint64_t gpuId, const std::string& bdf, int selfPid, const std::string& kfdRoot,

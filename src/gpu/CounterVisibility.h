@@ -125,7 +125,13 @@ class ProcScanCache {
   // this a job that exits looks like another namespace's process for that
   // long, and an auto-set daemon drops to its readable-only set for nothing.
   bool departing(int pid, uint64_t nowNs) const;
-  static constexpr uint64_t kDepartingGraceNs = 30'000'000'000ull;
+  // The same across PID namespaces (KFD's pids are not this /proc's): local
+  // processes that held memory on `bdf` at a full scan within the grace and
+  // hold none now (gone, or exiting) -- each may account for one KFD entry
+  // that no longer resolves.  A foreign process that starts on the GPU right
+  // after a local job left is noticed up to the grace later.
+  int departingStandIns(const std::string& bdf, uint64_t nowNs) const;
+  static constexpr uint64_t kDepartingGraceNs = 15'000'000'000ull;
   const std::string& procRoot() const { return procRoot_; }
   uint64_t reads() const { return reads_; }                  // /proc reads done (tests)
 
@@ -143,6 +149,7 @@ class ProcScanCache {
   uint64_t ttlNs_;
   std::map<int, Entry> by_;
   std::vector<LocalGpuProcess> all_;
+  std::map<int, std::pair<uint64_t, std::set<std::string>>> heldVram_;  // pid -> (last full scan seen, bdfs)
   uint64_t allNs_ = 0;
   bool haveAll_ = false;
   uint64_t lastPruneNs_ = 0;

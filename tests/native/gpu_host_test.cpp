@@ -1350,7 +1350,7 @@ TEST(GpuHost, ExitingJobIsDepartingNotForeign) {
   EXPECT_EQ(v.foreign, 0);
   EXPECT_TRUE(cache.departing(100, 12 * s));
   EXPECT_TRUE(cache.departing(200, 12 * s));
-  EXPECT_TRUE(gpuVisibility(12345, kBdfA, 400, procs, cache, 30 * s).full());
+  EXPECT_TRUE(gpuVisibility(12345, kBdfA, 400, procs, cache, 20 * s).full());
   // still listed long after the grace: counted as KFD processes not resolvable here
   v = gpuVisibility(12345, kBdfA, 400, procs, cache, 12 * s + ProcScanCache::kDepartingGraceNs + 2 * s);
   v = gpuVisibility(12345, kBdfA, 400, procs, cache, 12 * s + ProcScanCache::kDepartingGraceNs + 4 * s);
@@ -1358,4 +1358,35 @@ TEST(GpuHost, ExitingJobIsDepartingNotForeign) {
   EXPECT_EQ(v.foreign, 2);
   // the uncached check has no history: an exited job there is another namespace's
   EXPECT_FALSE(gpuVisibility(12345, kBdfA, 400, t.root + "/kfd", t.root + "/proc").full());
+}
+
+// The same across PID namespaces (the daemon in a container, as on the
+// gpurun boxes: KFD lists host pids, the job resolves through a local
+// stand-in).  When the job exits, its KFD entry outlives its local process;
+// the cache remembers the stand-in that held memory on the GPU and lets it
+// account for that entry during the grace.
+TEST(GpuHost, ExitingJobAcrossPidNamespacesIsDeparting) {
+  FakeTree t;
+  t.kfdProc(2823736, 555);  // the job (372 here)
+  t.kfdProc(2824005, 555);  // the daemon (400 here)
+  t.proc(372, kBdfA, 211184, "7f40-7f41 r--s 0 00:01 9 /memfd:dynolog-countable:555 (deleted)\n");
+  t.proc(400, kBdfA, 0, "");
+  t.put("proc/372/stat", "372 (python) S 1 372 372 0 -1 0 0 0 0 0 0 0 0 0 20 0 1 0 5000 0 0\n");
+  t.put("proc/400/stat", "400 (dynolog) S 1 400 400 0 -1 0 0 0 0 0 0 0 0 0 20 0 1 0 4000 0 0\n");
+  const uint64_t s = 1'000'000'000ull;
+  ProcScanCache cache(t.root + "/proc", 1 * s);
+  const auto procs = kfdProcesses(t.root + "/kfd");
+  auto v = gpuVisibility(555, kBdfA, 400, procs, cache, 10 * s);
+  EXPECT_TRUE(v.full());
+  ASSERT_EQ(v.pids.size(), 1u);
+  ASSERT_EQ(system(("rm -rf " + t.root + "/proc/372").c_str()), 0);  // gone here, KFD still lists it
+  v = gpuVisibility(555, kBdfA, 400, procs, cache, 12 * s);
+  EXPECT_TRUE(v.full());
+  EXPECT_EQ(v.foreign, 0);
+  EXPECT_EQ(cache.departingStandIns(kBdfA, 12 * s), 1);
+  EXPECT_TRUE(gpuVisibility(555, kBdfA, 400, procs, cache, 20 * s).full());
+  // past the grace an entry that still does not resolve is another namespace's
+  v = gpuVisibility(555, kBdfA, 400, procs, cache, 10 * s + ProcScanCache::kDepartingGraceNs + 3 * s);
+  EXPECT_FALSE(v.full());
+  EXPECT_EQ(v.foreign, 1);
 }

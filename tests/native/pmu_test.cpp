@@ -499,10 +499,13 @@ TEST(Pmu, PerProcessTargetCountsEveryThread) {
   const double msPerS = pm.lastOutputs().count("cpu_clock_ms_per_s") ? pm.lastOutputs().at("cpu_clock_ms_per_s") : 0.0;
   // The interval's counted CPU time is both workers' 2 x 150 ms (the main
   // thread sleeps in join): counting only one of them, or only the main
-  // thread, would give <= ~160 ms.  CPU time, so host load does not matter.
+  // thread, would give <= ~160 ms.  The upper bound only rules out counting
+  // a thread twice (>= ~560 ms): the main thread's own step() work and the
+  // scaling of the rate by a slightly different wall interval add up to
+  // ~140 ms on this VM (measured 398-443 ms in 4 of 20 runs).
   const double countedMs = msPerS * wallS;
   EXPECT_GT(countedMs, 260.0);
-  EXPECT_LT(countedMs, 360.0);
+  EXPECT_LT(countedMs, 520.0);
   pm.step();  // groups of the exited threads are gone: only the live threads remain
   // (the main thread, plus any runtime helper thread, e.g. TSAN's background thread)
   int live = 0;
