@@ -499,7 +499,10 @@ void Agent::sidecarLoop() {
     // samples its GPU itself.  A late heartbeat (a daemon that stalled or
     // died) is the stale path's to judge, not the rate's.
     const bool daemonPaused = sidecarReader_->header().paused.load(std::memory_order_relaxed) != 0;
-    if (sidecarGuard_.tick(now, sidecarReader_->head(), daemonPaused || hbAge > 200'000'000ull)) {
+    // (a window that closes inside a silence of the heartbeat -- a daemon
+    // killed a moment ago -- is the stale path's to judge, not the rate's)
+    if (sidecarGuard_.tick(now, sidecarReader_->head(), daemonPaused || hbAge > 200'000'000ull) &&
+        hbAge <= 20'000'000ull) {
       sidecarDeliveredHz_.store(sidecarGuard_.lastRateHz(), std::memory_order_relaxed);
       if (sidecarGuard_.low()) {
         sidecarRateLowWindows_++;
