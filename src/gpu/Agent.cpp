@@ -458,6 +458,7 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     R_ = sidecarReader_->rawStride();
     sidecarHaveLast_ = false;
     sidecarPciLoc_ = sidecarReader_->header().pci_loc;  // the GPU the daemon reads for us
+    sidecarHz_ = sidecarReader_->header().sample_hz;
     sidecarLost_ = sidecarReads_ = 0;
     sidecarStale_ = false;
     sidecarStaleEvents_ = 0;

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cmath>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -340,6 +341,10 @@ class Agent {
   mutable std::mutex sidecarMu_;                   // sidecarReader_ swaps (re-attach) against stats()
   bool sidecarReattach(uint64_t now);              // sampler thread: a restarted daemon's new segment
   std::string sidecarMismatch(const SlotBroadcastReader& r, const CounterPassSpec& want) const;
+  // a (restarted) daemon's target rate is the one this job attached to
+  // (within 0.5 %): a re-attach or hand-back never changes the job's rate
+  double sidecarHz_ = 0.0;  // sampler thread (set at start / join)
+  bool sameRate(double hz) const { return std::fabs(hz - sidecarHz_) <= 0.005 * sidecarHz_; }
   std::string samplerAutoReason_;                  // sampler "auto": why it chose what it chose
   uint64_t sidecarReducedSinceNs_ = 0;             // sampler thread
   std::atomic<uint64_t> sidecarStaleEvents_{0};    // outages seen

@@ -538,11 +538,12 @@ bool Agent::sidecarReattach(uint64_t now) {
   std::string e;
   auto r = SlotBroadcastReader::open(sidecarName_, &e);
   if (!r || !r->live(now, 1'000'000'000ull)) return false;  // not publishing yet: look again later
-  if (!r->carriesRaw() || !r->sameLayouts(*sidecarReader_)) {
+  if (!r->carriesRaw() || !r->sameLayouts(*sidecarReader_) || !sameRate(r->header().sample_hz)) {
     if (!sidecarReattachRefused_) {
       sidecarReattachRefused_ = true;
       LOG(WARNING) << "GPU agent: the restarted daemon (pid " << r->header().writer_pid << ") samples other counter "
-                   << "layouts on " << sidecarName_ << "; not re-attaching";
+                   << "layouts or another rate (" << r->header().sample_hz << " Hz) on " << sidecarName_
+                   << "; not re-attaching";
     }
     if (!fallbackPasses_.empty()) {
       if (sidecarFallback("the restarted daemon samples other counter sets", 1)) return true;
@@ -744,7 +745,8 @@ bool Agent::sidecarHandBack(uint64_t now) {
   if (sidecarReader_->replaced()) {
     std::string e;
     auto r = SlotBroadcastReader::open(sidecarName_, &e);
-    if (!r || !r->carriesRaw() || !r->sameLayouts(*sidecarReader_) || !r->live(now, 200'000'000ull)) {
+    if (!r || !r->carriesRaw() || !r->sameLayouts(*sidecarReader_) || !sameRate(r->header().sample_hz) ||
+        !r->live(now, 200'000'000ull)) {
       handBackGate_.observe(now, false, 0);
       return false;
     }
@@ -753,7 +755,8 @@ bool Agent::sidecarHandBack(uint64_t now) {
     sidecarReattaches_++;
   }
   const auto& h = sidecarReader_->header();
-  const bool healthy = sidecarReader_->live(now, 200'000'000ull) && h.full_set.load(std::memory_order_relaxed) != 0;
+  const bool healthy = sidecarReader_->live(now, 200'000'000ull) && h.full_set.load(std::memory_order_relaxed) != 0 &&
+                       sameRate(h.sample_hz);
   if (!handBackGate_.observe(now, healthy, sidecarReader_->head())) return false;
   sampler_->stop();
   {
@@ -870,6 +873,7 @@ bool Agent::sidecarJoin(uint64_t now) {
   sidecarReader_->skipToHead();
   sidecarRaw_ = true;
   sidecarPciLoc_ = sidecarReader_->header().pci_loc;
+  sidecarHz_ = sidecarReader_->header().sample_hz;
   sidecarHaveLast_ = false;
   sidecarStale_ = false;
   sidecarReducedSinceNs_ = 0;
