@@ -1189,6 +1189,7 @@ def _main(args, wd) -> int:
                     # when the first exceeds the second)
                     "sidecar_takeovers": st.get("sidecar_takeovers"),
                     "sidecar_handbacks": st.get("sidecar_handbacks"),
+                    "sidecar_joins": st.get("sidecar_joins"),
                     "gather_latency_us_avg": round(st.get("gather_latency_us_avg", 0.0), 2),
                     "gathers": st.get("gathers")}
             ranks = [None] * env.world
@@ -1213,7 +1214,7 @@ def _main(args, wd) -> int:
                              "sidecar_fell_back", "sidecar_fallback_after_ms", "sidecar_fallback_cause",
                              "sidecar_delivered_hz", "sidecar_rate_low_windows", "sidecar_reattaches",
                              "sampler_auto_reason", "step_stage_slots", "step_stage_grows",
-                             "sidecar_takeovers", "sidecar_handbacks")
+                             "sidecar_takeovers", "sidecar_handbacks", "sidecar_joins")
                             if k in agent_stats}
             out["agent"]["host_rss_mb_after_warmup"] = rss_start
         if args.sampler == "daemon" and env.local_rank == 0:
