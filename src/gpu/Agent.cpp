@@ -986,7 +986,8 @@ void Agent::controlLoop() {
   uint64_t nextKeepalive = 0;
   while (!stopFlag_) {
     const uint64_t now = monoNs();
-    if (now >= nextKeepalive) {
+    // a takeover, hand-back or join is told at once (the sampler thread sets it)
+    if (now >= nextKeepalive || ctlStateChanged_.exchange(false)) {
       Json c = Json::object();
       c["pid"] = pid;
       c["rank"] = cfg_.jobRank();
@@ -996,6 +997,18 @@ void Agent::controlLoop() {
       c["thread_trace"] = ThreadTracer::get().configured();
       c["dispatch_counters"] = DispatchCounters::get().configured();
       c["comm_trace"] = CommTracer::get().configured();
+      Json sm = Json::object();
+      const bool inProcess = !sidecar_.load() || sidecarFellBack_.load();
+      sm["sampler"] = inProcess ? "agent" : "daemon";
+      sm["sampler_requested"] = samplerRequested_;
+      sm["sample_hz"] = cfg_.sampleHz;
+      sm["samples_taken"] = static_cast<unsigned long long>(samplesTaken_.load());
+      if (sidecar_.load() || samplerRequested_ != "agent") {
+        sm["sidecar_takeovers"] = static_cast<unsigned long long>(sidecarTakeovers_.load());
+        sm["sidecar_handbacks"] = static_cast<unsigned long long>(sidecarHandBacks_.load());
+        sm["sidecar_joins"] = static_cast<unsigned long long>(sidecarJoins_.load());
+      }
+      c["sampling"] = sm;
       (void)ctl_->syncSend(ipc::Message::fromString(ipc::kMsgAgentContext, c.dump()), cfg_.daemonEndpoint, 1, 0);
       nextKeepalive = now + 10'000'000'000ull;
     }

@@ -326,6 +326,7 @@ class Agent {
   uint32_t stepPassCap_ = 0;       // entries allocated in dStepPasses_
   HandBackGate handBackGate_;                      // sampler thread
   std::atomic<uint64_t> sidecarTakeovers_{0}, sidecarHandBacks_{0};
+  std::atomic<bool> ctlStateChanged_{false};       // the control thread re-announces at once
   std::atomic<uint64_t> sidecarHandBackHoldNs_{0};
   // why it fell back: 1 the daemon stopped publishing (or was restarted with
   // other counter sets), 2 it dropped to its readable-only set (an

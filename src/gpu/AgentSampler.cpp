@@ -724,6 +724,7 @@ bool Agent::sidecarFallback(const char* why, int cause) {
   sidecarFallbackNs_ = monoNs();
   sidecarFallbackCause_ = cause;
   sidecarTakeovers_++;
+  ctlStateChanged_ = true;
   handBackGate_.reset();
   handBackGate_.setTarget(sidecarReader_->header().sample_hz, kSidecarMinRateFraction);
   sidecarFellBack_ = true;
@@ -772,6 +773,7 @@ bool Agent::sidecarHandBack(uint64_t now) {
   sidecarStale_ = false;
   sidecarReducedSinceNs_ = 0;
   sidecarHandBacks_++;
+  ctlStateChanged_ = true;
   sidecarHandBackHoldNs_ = handBackGate_.holdNs();
   sidecarFellBack_ = false;
   LOG(WARNING) << "GPU agent: the daemon's broadcast " << sidecarName_ << " is healthy again (writer pid "
@@ -882,6 +884,7 @@ bool Agent::sidecarJoin(uint64_t now) {
   sidecarFellBack_ = false;
   sidecarJoins_++;
   sidecar_ = true;
+  ctlStateChanged_ = true;
   LOG(WARNING) << "GPU agent: the daemon's broadcast " << sidecarName_ << " is live with this job's set and rate ("
                << joinGate_.lastRateHz() << " samples/s over " << joinGate_.holdNs() / 2000000000ull
                << " s); sampling through it from now on";

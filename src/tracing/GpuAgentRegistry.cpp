@@ -70,6 +70,7 @@ void GpuAgentRegistry::onContext(const Json& j, const std::string& src) {
   e.dispatchCounters = j.contains("dispatch_counters") && j.at("dispatch_counters").isBool() &&
                        j.at("dispatch_counters").asBool();
   e.commTrace = j.contains("comm_trace") && j.at("comm_trace").isBool() && j.at("comm_trace").asBool();
+  if (j.contains("sampling") && j.at("sampling").isObject()) e.sampling = j.at("sampling");
   e.lastSeenNs = nowNsMonotonic();
   if (e.pid <= 0) return;
   std::lock_guard<std::mutex> g(mu_);
@@ -121,6 +122,7 @@ Json GpuAgentRegistry::listJson() {
     o["thread_trace"] = e.threadTrace;
     o["dispatch_counters"] = e.dispatchCounters;
     o["comm_trace"] = e.commTrace;
+    if (e.sampling.isObject()) o["sampling"] = e.sampling;
     o["last_seen_s"] = (now - e.lastSeenNs) * 1e-9;
     arr.push_back(o);
   }

@@ -34,6 +34,9 @@ struct GpuAgentEntry {
   bool threadTrace = false;
   bool dispatchCounters = false;
   bool commTrace = false;
+  // who reads this agent's GPU counters, as of its last keepalive ("sampler":
+  // agent / daemon, and the sidecar's takeovers, hand-backs and joins)
+  Json sampling;
   uint64_t lastSeenNs = 0;
 };
 
