@@ -14,4 +14,5 @@ for r in d.get("rows", []):
     print(json.dumps({k: r.get(k) for k in ("entry", "rc", "samples_per_sec", "ms_per_step", "pooled_overhead_pct",
                                             "overhead_vs_no_agent_pct", "sample_latency_us_avg")}))
 print(json.dumps({"countable_only_vs_no_agent_pct": d.get("countable_only_vs_no_agent_pct")}))
-PYexit $rc
+PY
+exit $rc
