@@ -733,10 +733,9 @@ def _main(args, wd) -> int:
     ag = None
     sidecar = None  # the node's daemon (sampler daemon, local rank 0)
     sidecar_fallback = None
-    if use_agent and args.sampler == "daemon" and (args.counter_passes or args.sweep_hz):
-        # the daemon samples one counter set at one rate; pass rotation and the
-        # rate sweep are the in-process agent's
-        sidecar_fallback = "--counter-passes / --sweep-hz sample in process"
+    if use_agent and args.sampler == "daemon" and args.sweep_hz:
+        # the daemon samples at one rate; the rate sweep is the in-process agent's
+        sidecar_fallback = "--sweep-hz samples in process"
         args.sampler = "agent"
     if use_agent and args.sampler == "daemon":
         wd.phase("sidecar daemon start", 120.0)
@@ -744,9 +743,11 @@ def _main(args, wd) -> int:
         if env.local_rank == 0:
             try:
                 from dynolog_amd.utils.daemon import DaemonProcess
-                sidecar = DaemonProcess(["--enable_gpu_counters", f"--gpu_counter_hz={args.sample_hz}",
-                                         f"--gpu_counters={args.counter_set}",
-                                         "--gpu_counter_reporting_interval_s=3600"]).start()
+                dflags = ["--enable_gpu_counters", f"--gpu_counter_hz={args.sample_hz}",
+                          f"--gpu_counters={args.counter_set}", "--gpu_counter_reporting_interval_s=3600"]
+                if args.counter_passes:  # the daemon rotates the same plan; the agents take its layouts
+                    dflags.append(f"--gpu_counter_passes={args.counter_passes}")
+                sidecar = DaemonProcess(dflags).start()
                 deadline = time.time() + 60
                 mon = {}
                 while time.time() < deadline:

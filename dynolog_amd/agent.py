@@ -498,7 +498,9 @@ class GpuAgent:
         job that started in process likewise joins a daemon that comes up
         later, at its set and rate (``sidecar_joins``).  With sampler "auto" the daemon
         is taken only when its broadcast is live, on the full set, at this
-        job's ``sample_hz`` and ``counter_set`` (stats ``sampler_auto_reason``)."""
+        job's ``sample_hz`` and ``counter_set`` -- with ``counter_passes``,
+        when the daemon rotates every one of the job's passes
+        (``dynolog --gpu_counter_passes``) -- (stats ``sampler_auto_reason``)."""
         if not _preinit_done:
             raise AgentError("dynolog_amd.agent.preinit() must be called before HIP init")
         lib = _native.load_gpu_lib()

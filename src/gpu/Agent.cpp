@@ -185,8 +185,12 @@ bool Agent::setupLayout(PassState& ps, const std::vector<uint64_t>& ids, std::st
 
 // "" when the daemon's broadcast can stand in for this process's own
 // sampling: live (heartbeat < 1 s, not paused), on its full set, sampling
-// the counter set and rate this job asked for; else why not.
-std::string Agent::sidecarMismatch(const SlotBroadcastReader& r, const CounterPassSpec& want) const {
+// the counter set and rate this job asked for -- with a pass plan
+// (counter_passes), the daemon's first pass is the job's first and every
+// pass of the job is among the daemon's layouts (the daemon's own plan,
+// --gpu_counter_passes, sets the rotation); else why not.
+std::string Agent::sidecarMismatch(const SlotBroadcastReader& r, const std::vector<CounterPassSpec>& specs) const {
+  const CounterPassSpec& want = specs.at(0);
   const auto& h = r.header();
   char b[200];
   if (!r.live(monoNs(), 1'000'000'000ull)) return "the daemon's broadcast is not live (stale heartbeat or paused)";
@@ -206,6 +210,17 @@ std::string Agent::sidecarMismatch(const SlotBroadcastReader& r, const CounterPa
     snprintf(b, sizeof(b), "the daemon samples counter set (pass %u, mask 0x%x), this job asked for '%s' (pass %u, mask 0x%x)",
              h.main_pass, h.main_counter_mask, want.set.c_str(), want.pass, mask);
     return b;
+  }
+  for (size_t i = 1; i < specs.size(); ++i) {
+    const uint32_t m = selectedCounterMask(specs[i].names);
+    bool found = false;
+    for (uint32_t k = 0; k < r.layoutCount() && !found; ++k)
+      found = r.layout(k).pass == specs[i].pass && r.layout(k).counter_mask == m;
+    if (!found) {
+      snprintf(b, sizeof(b), "the daemon does not rotate through this job's pass '%s' (pass %u, mask 0x%x)",
+               specs[i].set.c_str(), specs[i].pass, m);
+      return b;
+    }
   }
   return "";
 }
@@ -419,16 +434,15 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
     const std::string name = cfg_.sidecarRing.empty() ? slotBroadcastName(pciLoc_) : cfg_.sidecarRing;
     std::unique_ptr<SlotBroadcastReader> r;
     if (!stepPack_) samplerAutoReason_ = "pack_mode " + cfg_.packMode + " samples in process";
-    else if (!cfg_.counterPasses.empty()) samplerAutoReason_ = "counter_passes rotate sets in process";
     else if (!(r = SlotBroadcastReader::open(name, &e))) samplerAutoReason_ = e;
-    else samplerAutoReason_ = sidecarMismatch(*r, specs[0]);
+    else samplerAutoReason_ = sidecarMismatch(*r, specs);
     sidecar_ = r && samplerAutoReason_.empty();
     if (sidecar_) samplerAutoReason_ = "the daemon's broadcast is live with this job's set and rate";
     cfg_.sampler = sidecar_ ? "daemon" : "agent";
     LOG(INFO) << "GPU agent: sampler auto -> " << cfg_.sampler << " (" << samplerAutoReason_ << ")";
     // in process for now: a daemon that comes up later (or catches up with
     // this job's rate) is joined once healthy (sidecar_handback)
-    autoJoin_ = !sidecar_ && stepPack_ && cfg_.counterPasses.empty() && cfg_.sidecarHandBack;
+    autoJoin_ = !sidecar_ && stepPack_ && cfg_.sidecarHandBack;
   } else {
     autoJoin_ = false;
   }

@@ -341,7 +341,7 @@ class Agent {
   bool sidecarReattachRefused_ = false;            // sampler thread: warned once
   mutable std::mutex sidecarMu_;                   // sidecarReader_ swaps (re-attach) against stats()
   bool sidecarReattach(uint64_t now);              // sampler thread: a restarted daemon's new segment
-  std::string sidecarMismatch(const SlotBroadcastReader& r, const CounterPassSpec& want) const;
+  std::string sidecarMismatch(const SlotBroadcastReader& r, const std::vector<CounterPassSpec>& specs) const;
   // a (restarted) daemon's target rate is the one this job attached to
   // (within 0.5 %): a re-attach or hand-back never changes the job's rate
   double sidecarHz_ = 0.0;  // sampler thread (set at start / join)

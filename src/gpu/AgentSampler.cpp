@@ -798,7 +798,9 @@ bool Agent::sidecarJoin(uint64_t now) {
   const SlotBroadcastReader& r = *joinReader_;
   const uint32_t own = static_cast<uint32_t>(passes_.size());
   const bool fits = r.carriesRaw() && static_cast<int>(r.rawStride()) <= stepStride_ && own + r.layoutCount() <= stepPassCap_;
-  const bool healthy = fits && sidecarMismatch(r, passes_[0].spec).empty();
+  std::vector<CounterPassSpec> specs;
+  for (const auto& ps : passes_) specs.push_back(ps.spec);
+  const bool healthy = fits && sidecarMismatch(r, specs).empty();
   if (!joinGate_.observe(now, healthy, r.head())) return false;
   // the daemon's layouts as pass-table entries [own, own + layouts)
   std::string e;

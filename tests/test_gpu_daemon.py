@@ -752,6 +752,62 @@ def test_sidecar_auto_joins_a_daemon_started_later(native_built):
                     pass
 
 
+def test_sidecar_auto_takes_a_daemon_rotating_the_jobs_pass_plan(native_built):
+    """A job with a pass plan (counter_passes "lite:3,mfma:1") and sampler
+    "auto" takes the daemon's read when the daemon rotates the same passes
+    (--gpu_counter_passes): its records carry both passes' metrics
+    (sm_occupancy from lite, mfma_f8_tflops from the mfma pass) with no
+    counting context of its own; a job whose plan the daemon does not rotate samples in process and
+    says which pass is missing."""
+    code = textwrap.dedent("""
+        from dynolog_amd import agent
+        agent.preinit()
+        import json, sys, time, torch
+        a = agent.GpuAgent.start(device=0, sample_hz=1000, sinks=("memory",), log_interval_ms=100,
+                                 sampler="auto", counter_passes=sys.argv[1])
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        end = time.time() + 2.5
+        while time.time() < end:
+            for _ in range(8):
+                y = x @ x
+            a.step(); torch.cuda.synchronize()
+        a.step(catch_up=True); torch.cuda.synchronize(); a.flush(); time.sleep(0.3)
+        recs = [r for r in a.memory_records() if "phase" not in r]
+        st = a.stats(); a.stop()
+        print("RESULT " + json.dumps({"sampler": st["sampler"], "reason": st.get("sampler_auto_reason"),
+                                      "samples": st["samples_taken"], "failed": st["samples_failed"],
+                                      "lite": sum(1 for r in recs if "sm_occupancy" in r),
+                                      "mfma": sum(1 for r in recs if "mfma_f8_tflops" in r)}), flush=True)
+    """)
+    d = DaemonProcess(["--enable_gpu_counters", "--gpu_counter_hz=1000", "--gpu_counters=lite",
+                       "--gpu_counter_passes=lite:3,mfma:1"]).start()
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            mon = d.rpc({"fn": "getGpuCounterMonitor"})
+            g0 = (mon.get("gpus") or [{}])[0]
+            if mon.get("status") == "ok" and g0.get("slots_published", 0) > 100 and g0.get("sample_hz_achieved", 0) > 0:
+                break
+            time.sleep(0.2)
+        res = {}
+        for plan in ("lite:3,mfma:1", "lite:3,precision:1"):
+            r = subprocess.run([sys.executable, "-c", code, plan], capture_output=True, text=True, timeout=240,
+                               env=dict(os.environ, PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+            lines = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+            assert r.returncode == 0 and lines, r.stderr[-3000:]
+            res[plan] = json.loads(lines[-1][7:])
+        print(json.dumps(res))
+        same = res["lite:3,mfma:1"]
+        assert same["sampler"] == "daemon" and "live with this job" in same["reason"], same
+        assert same["samples"] > 1500 and same["failed"] == 0, same
+        assert same["lite"] > 0 and same["mfma"] > 0, same  # both passes' records
+        other = res["lite:3,precision:1"]
+        assert other["sampler"] == "agent" and "does not rotate through this job's pass 'precision'" in other["reason"], other
+        assert other["samples"] > 1500 and other["lite"] > 0, other
+    finally:
+        d.stop()
+
+
 def test_sidecar_takes_over_when_the_daemon_reduces_its_set(native_built):
     """A daemon on the default "auto" set drops to the readable-only `xproc`
     set while an uncountable job shares the GPU.  A sidecar job on that GPU
