@@ -408,6 +408,8 @@ bool Agent::start(const AgentConfig& cfg, const void* uid, size_t idLen, std::st
   handBackGate_ = HandBackGate();
   sidecarTakeovers_ = sidecarHandBacks_ = 0;
   sidecarHandBackHoldNs_ = handBackGate_.holdNs();
+  handBackResets_ = handBackShortHolds_ = 0;
+  handBackLastRateHz_ = 0.0;
   sidecarFallbackNs_ = 0;
   sidecarFallbackCause_ = 0;
   sidecarReducedSinceNs_ = 0;
@@ -1631,6 +1633,11 @@ Json Agent::stats() const {
     j["sidecar_handbacks"] = static_cast<unsigned long long>(sidecarHandBacks_.load());
     j["sidecar_handback"] = cfg_.sidecarHandBack;
     j["sidecar_handback_hold_ms"] = sidecarHandBackHoldNs_.load() * 1e-6;
+    // why a hand-back has not happened yet: holds cut short by an unhealthy
+    // check (stale, paused, reduced set, other rate) or short of the rate
+    j["sidecar_handback_resets"] = static_cast<unsigned long long>(handBackResets_.load());
+    j["sidecar_handback_short_holds"] = static_cast<unsigned long long>(handBackShortHolds_.load());
+    j["sidecar_handback_last_rate_hz"] = handBackLastRateHz_.load();
     if (sidecarTakeovers_.load() > 0) {  // the latest takeover
       j["sidecar_fallback_after_ms"] = (sidecarFallbackNs_.load() - startNs_) * 1e-6;
       const int cause = sidecarFallbackCause_.load();

@@ -328,6 +328,9 @@ class Agent {
   std::atomic<uint64_t> sidecarTakeovers_{0}, sidecarHandBacks_{0};
   std::atomic<bool> ctlStateChanged_{false};       // the control thread re-announces at once
   std::atomic<uint64_t> sidecarHandBackHoldNs_{0};
+  // the hand-back gate's view for stats (the gate itself is the sampler thread's)
+  std::atomic<uint64_t> handBackResets_{0}, handBackShortHolds_{0};
+  std::atomic<double> handBackLastRateHz_{0.0};
   // why it fell back: 1 the daemon stopped publishing (or was restarted with
   // other counter sets), 2 it dropped to its readable-only set (an
   // uncountable process joined the GPU), 3 it published less than

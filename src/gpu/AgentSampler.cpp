@@ -758,7 +758,11 @@ bool Agent::sidecarHandBack(uint64_t now) {
   const auto& h = sidecarReader_->header();
   const bool healthy = sidecarReader_->live(now, 200'000'000ull) && h.full_set.load(std::memory_order_relaxed) != 0 &&
                        sameRate(h.sample_hz);
-  if (!handBackGate_.observe(now, healthy, sidecarReader_->head())) return false;
+  const bool pass = handBackGate_.observe(now, healthy, sidecarReader_->head());
+  handBackResets_ = handBackGate_.resets();
+  handBackShortHolds_ = handBackGate_.shortHolds();
+  handBackLastRateHz_ = handBackGate_.lastRateHz();
+  if (!pass) return false;
   sampler_->stop();
   {
     std::lock_guard<std::mutex> g(passesMu_);

@@ -494,6 +494,7 @@ class HandBackGate {
   // now.  head: the broadcast's published count.
   bool observe(uint64_t nowNs, bool healthy, uint64_t head) {
     if (!healthy || nowNs < since_ || (since_ != 0 && head < head0_)) {
+      if (since_ != 0) ++resets_;
       since_ = 0;
       return false;
     }
@@ -506,6 +507,7 @@ class HandBackGate {
     const double rate = static_cast<double>(head - head0_) * 1e9 / static_cast<double>(nowNs - since_);
     lastRateHz_ = rate;
     if (rate < minFraction_ * hz_) {  // short over the hold: a new hold from here
+      ++shortHolds_;
       since_ = nowNs;
       head0_ = head;
       return false;
@@ -516,12 +518,15 @@ class HandBackGate {
   }
   uint64_t holdNs() const { return hold_; }  // the next hand-back's
   double lastRateHz() const { return lastRateHz_; }  // over the last completed hold
+  uint64_t resets() const { return resets_; }           // holds cut short by an unhealthy check
+  uint64_t shortHolds() const { return shortHolds_; }   // holds that ran short of the rate
 
  private:
   double hz_, minFraction_;
   uint64_t hold_, maxHold_;
   uint64_t since_ = 0, head0_ = 0;
   double lastRateHz_ = 0.0;
+  uint64_t resets_ = 0, shortHolds_ = 0;
 };
 
 class BroadcastRateGuard {
