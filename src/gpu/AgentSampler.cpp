@@ -756,8 +756,10 @@ bool Agent::sidecarHandBack(uint64_t now) {
     sidecarReattaches_++;
   }
   const auto& h = sidecarReader_->header();
+  // (rate_mhz != 0: the daemon has sampled a full second -- a daemon that
+  // just started has a slow first second, which no hold should average in)
   const bool healthy = sidecarReader_->live(now, 200'000'000ull) && h.full_set.load(std::memory_order_relaxed) != 0 &&
-                       sameRate(h.sample_hz);
+                       sameRate(h.sample_hz) && h.rate_mhz.load(std::memory_order_relaxed) != 0;
   const bool pass = handBackGate_.observe(now, healthy, sidecarReader_->head());
   handBackResets_ = handBackGate_.resets();
   handBackShortHolds_ = handBackGate_.shortHolds();
@@ -804,7 +806,7 @@ bool Agent::sidecarJoin(uint64_t now) {
   const bool fits = r.carriesRaw() && static_cast<int>(r.rawStride()) <= stepStride_ && own + r.layoutCount() <= stepPassCap_;
   std::vector<CounterPassSpec> specs;
   for (const auto& ps : passes_) specs.push_back(ps.spec);
-  const bool healthy = fits && sidecarMismatch(r, specs).empty();
+  const bool healthy = fits && r.header().rate_mhz.load(std::memory_order_relaxed) != 0 && sidecarMismatch(r, specs).empty();
   if (!joinGate_.observe(now, healthy, r.head())) return false;
   // the daemon's layouts as pass-table entries [own, own + layouts)
   std::string e;

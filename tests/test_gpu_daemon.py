@@ -677,7 +677,7 @@ def test_sidecar_hands_back_to_a_restarted_daemon(native_built):
             time.sleep(4.5)  # stale after 3 s: the job samples in process
             d2 = DaemonProcess(args).start()
             assert wait_publishing(d2), d2.log()[-3000:]
-            time.sleep(7.5)  # its first full second, the 3 s hold, then 2 s through it
+            time.sleep(9.0)  # its first full second, the 3 s hold, then 2 s through it (and slack)
             rc = c.finish(flag, timeout=60)
             res = [json.loads(l[7:]) for l in c.lines("RESULT ")]
             assert rc == 0 and res, c.tails()
@@ -723,7 +723,7 @@ def test_sidecar_auto_joins_a_daemon_started_later(native_built):
                 if mon.get("status") == "ok" and mon["gpus"][0].get("slots_published", 0) > 100:
                     break
                 time.sleep(0.2)
-            time.sleep(7.0)  # its first full second, the 3 s hold, then a few seconds through it
+            time.sleep(8.0)  # its first full second, the 3 s hold, then a few seconds through it
             d.proc.kill()
             d.proc.wait(timeout=30)
             time.sleep(3.0)  # taken back within ~0.1 s: the last 2 s are the job's own
