@@ -32,6 +32,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="agent", choices=["none", "countable", "preinit", "preinit_nodev", "agent", "daemon"])
     ap.add_argument("--secs", type=float, default=4.0)
+    ap.add_argument("--no-kernel", action="store_true", help="initialise the GPU but launch no kernel (no HIP queue yet)")
+    ap.add_argument("--syscalls", type=int, default=0,
+                    help="read the busiest thread's /proc syscall file this many times; count (nr, arg1) pairs")
     a = ap.parse_args()
     d = None
     if a.mode == "countable":  # libdyno_countable.so: a counting context configured, never started
@@ -45,8 +48,12 @@ def main():
         agent.preinit()
     import torch
     torch.cuda.set_device(0)
-    x = torch.randn(1024, 1024, device="cuda")
-    (x @ x).sum().item()
+    if a.no_kernel:
+        torch.cuda.init()
+        torch.empty(1 << 20, device="cuda")  # an allocation, no dispatch
+    else:
+        x = torch.randn(1024, 1024, device="cuda")
+        (x @ x).sum().item()
     ag = None
     if a.mode == "daemon":
         from dynolog_amd.utils.daemon import DaemonProcess
@@ -74,6 +81,27 @@ def main():
         if n > 0:
             from collections import Counter
             pcs = Counter(buf.value.decode().split("\n")[:-1]).most_common(8)
+    # what the busiest thread asks the kernel for: its syscall number and first
+    # two arguments (for an ioctl, the fd and the request code), read N times
+    calls = []
+    if rows and a.syscalls > 0:
+        from collections import Counter
+        c = Counter()
+        for _ in range(a.syscalls):
+            try:
+                f = open(f"/proc/{pid}/task/{rows[0][1]}/syscall").read().split()
+            except OSError:
+                break
+            c[" ".join(f[:3])] += 1
+        for k, n in c.most_common(8):
+            f = k.split()
+            target = None
+            if len(f) >= 2 and f[0] == "16":  # ioctl: name the fd
+                try:
+                    target = os.readlink(f"/proc/{pid}/fd/{int(f[1], 16)}")
+                except (OSError, ValueError):
+                    pass
+            calls.append([k, n, target])
     st = ag.stats() if ag else {}
     if ag:
         ag.stop()
@@ -82,7 +110,8 @@ def main():
     print(json.dumps({"mode": a.mode, "total_pct": round(sum(r[0] for r in rows), 1),
                       "threads": [{"tid": t, "name": n, "cpu_pct": round(c, 1), "syscall": sc, "wchan": w}
                                   for c, t, n, sc, w in rows[:6]],
-                      "busiest_thread_pcs": pcs, "samples_taken": st.get("samples_taken")}))
+                      "busiest_thread_pcs": pcs, "busiest_thread_syscalls": calls,
+                      "no_kernel": a.no_kernel, "samples_taken": st.get("samples_taken")}))
 
 
 if __name__ == "__main__":
