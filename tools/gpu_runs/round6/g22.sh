@@ -11,3 +11,6 @@ timeout -k 10 120 python -u $P --mode countable --syscalls 20000 > $O/countable.
 timeout -k 10 120 python -u $P --mode countable --no-kernel --syscalls 20000 > $O/countable_nokernel.json 2> $O/countable_nokernel.err || exit $?
 timeout -k 10 120 python -u $P --mode preinit --syscalls 20000 > $O/preinit.json 2> $O/preinit.err || exit $?
 cat $O/*.json
+# the runtime's own WaitAny trace in a countable process (first 1 MB of it)
+(HSA_WAIT_ANY_DEBUG=1 timeout -k 10 60 python -u $P --mode countable --secs 1 2>&1 >/dev/null | head -c 1000000 > $O/countable_waitany.txt) || true
+wc -l $O/countable_waitany.txt; head -c 1500 $O/countable_waitany.txt
