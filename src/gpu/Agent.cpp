@@ -1612,6 +1612,8 @@ Json Agent::stats() const {
   j["log_intervals_dropped"] = static_cast<unsigned long long>(logDropped_.load());
   j["pack_mode"] = cfg_.packMode;
   j["sampler"] = sidecar_.load() ? "daemon" : "agent";  // (after a late join: daemon)
+  // other GPUs made countable with a never-started counting service (RocprofSampler.cpp)
+  j["countable_other_gpus"] = RocprofRuntime::get().markOnlyContexts();
   j["sidecar_joins"] = static_cast<unsigned long long>(sidecarJoins_.load());
   j["sampler_requested"] = samplerRequested_;
   if (!samplerAutoReason_.empty()) j["sampler_auto_reason"] = samplerAutoReason_;

@@ -70,6 +70,9 @@ class RocprofRuntime {
   // Context for an agent index, or -1 if not configured.
   bool hasContext(int agentIndex) const;
   std::string lastError() const { return err_; }
+  // GPUs outside `devices` whose counting service is configured only to make
+  // this process's waves countable there (never started)
+  int markOnlyContexts() const { return markOnlyContexts_; }
 
   // --- internal, used by the tool-init callback ---
   int toolInit();
@@ -92,6 +95,7 @@ class RocprofRuntime {
   bool commTrace_ = false;
   std::vector<AgentInfo> agents_;
   std::map<int, std::unique_ptr<Ctx>> ctxs_;
+  int markOnlyContexts_ = 0;
   std::string err_;
 };
 

@@ -981,6 +981,45 @@ TEST(GpuHost, VisibilityAcrossPidNamespaces) {
   EXPECT_EQ(v.uncountable[0], 372);
 }
 
+// Two DDP ranks on two GPUs, the daemon in another PID namespace: each rank
+// holds its peer's RCCL buffers (megabytes) on the peer GPU without a queue
+// there, so on that GPU it stands in like a compute process.  Marked
+// countable on its own GPU only (the agent before round 6), it made every
+// peer GPU look uncountable; marked on every GPU of the node (the agent's
+// never-started services on the other GPUs, RocprofSampler.cpp) both GPUs
+// stay on the full set.
+TEST(GpuHost, DdpPeerBuffersKeepTheFullSetWhenMarkedOnEveryGpu) {
+  FakeTree t;
+  t.kfdProc(3000001, 555);  // rank 0's queue on GPU A
+  t.kfdProc(3000002, 777);  // rank 1's queue on GPU B
+  t.kfdProc(3000009, 555);  // the daemon
+  t.kfdProc(3000009, 777);
+  auto peerFd = [&](int pid, const std::string& bdf, uint64_t kib) {
+    const std::string p = "proc/" + std::to_string(pid);
+    t.link(p + "/fd/8", "/dev/dri/renderD136");
+    t.put(p + "/fdinfo/8", "pos:\t0\ndrm-driver:\tamdgpu\ndrm-pdev:\t" + bdf + "\ndrm-total-vram:\t" +
+                               std::to_string(kib) + " KiB\n");
+  };
+  t.proc(10, kBdfA, 180000, "7f40-7f41 r--s 0 00:01 9 /memfd:dynolog-countable:555 (deleted)\n");
+  peerFd(10, kBdfB, 8192);
+  t.proc(11, kBdfB, 180000, "7f40-7f41 r--s 0 00:01 9 /memfd:dynolog-countable:777 (deleted)\n");
+  peerFd(11, kBdfA, 8192);
+  t.proc(400, kBdfA, 0, "");
+  auto a = gpuVisibility(555, kBdfA, 400, t.root + "/kfd", t.root + "/proc");
+  ASSERT_EQ(a.uncountable.size(), 1u);  // rank 1, by its peer buffers on A
+  EXPECT_EQ(a.uncountable[0], 11);
+  EXPECT_FALSE(a.full());
+  EXPECT_FALSE(gpuVisibility(777, kBdfB, 400, t.root + "/kfd", t.root + "/proc").full());
+  // each rank marked on both GPUs
+  t.put("proc/10/maps", "7f40-7f41 r--s 0 00:01 9 /memfd:dynolog-countable:555,777 (deleted)\n");
+  t.put("proc/11/maps", "7f40-7f41 r--s 0 00:01 9 /memfd:dynolog-countable:777,555 (deleted)\n");
+  a = gpuVisibility(555, kBdfA, 400, t.root + "/kfd", t.root + "/proc");
+  EXPECT_TRUE(a.uncountable.empty());
+  EXPECT_EQ(a.foreign, 0);
+  EXPECT_TRUE(a.full());
+  EXPECT_TRUE(gpuVisibility(777, kBdfB, 400, t.root + "/kfd", t.root + "/proc").full());
+}
+
 TEST(GpuHost, CountableMarkIsSeenInOwnMaps) {
   EXPECT_TRUE(dynoMarkCountable({42, 4242}));
   EXPECT_TRUE(processCountable(static_cast<int>(getpid()), 4242));

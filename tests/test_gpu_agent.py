@@ -726,6 +726,9 @@ def test_agent_index_under_visible_devices(native_built):
     assert res["idx"] == 0 and res["n"] == 1, res
     st = res["st"]
     assert st["samples_taken"] > 500 and st["samples_failed"] == 0 and st["last_error"] == "", st
+    # every other visible GPU gets a never-started service that marks this
+    # process countable there (none on a one-GPU list)
+    assert st["countable_other_gpus"] == res["n"] - 1, st
 
 
 def test_step_inside_graph_capture_is_skipped(native_built):
