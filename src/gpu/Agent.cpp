@@ -1575,6 +1575,11 @@ Json Agent::stats() const {
   j["collective"] = collective_;
   j["device"] = cfg_.device;
   j["sample_hz_target"] = cfg_.sampleHz;
+  // one order for the three counters the sampler and step() advance: packed
+  // <= staged <= taken holds at every instant, so read packed, then staged,
+  // then taken and the snapshot keeps it
+  const uint64_t packedSnap = stagePacked_.load();
+  const uint64_t stagedSnap = stepHead_.load();
   j["samples_taken"] = static_cast<unsigned long long>(samplesTaken_.load());
   j["samples_failed"] = static_cast<unsigned long long>(samplesFailed_.load());
   j["batches"] = static_cast<unsigned long long>(batches_.load());
@@ -1677,8 +1682,8 @@ Json Agent::stats() const {
     j["step_stage_max_slots"] = static_cast<unsigned long long>(stageMaxSlots_);
     j["step_stage_grows"] = static_cast<unsigned long long>(stageGrows_.load());
     j["step_stage_grow_failures"] = static_cast<unsigned long long>(stageGrowFails_.load());
-    j["step_staged"] = static_cast<unsigned long long>(stepHead_.load());
-    j["step_packed"] = static_cast<unsigned long long>(stagePacked_.load());
+    j["step_staged"] = static_cast<unsigned long long>(stagedSnap);
+    j["step_packed"] = static_cast<unsigned long long>(packedSnap);
     j["step_stage_full_ticks"] = static_cast<unsigned long long>(stageFull_.load());
   }
   // trainer-stream time of a gather (gather_prep + size all-reduce + collective)
