@@ -749,16 +749,26 @@ def _main(args, wd) -> int:
                     dflags.append(f"--gpu_counter_passes={args.counter_passes}")
                 sidecar = DaemonProcess(dflags).start()
                 deadline = time.time() + 60
+                rate_deadline = None
                 mon = {}
                 while time.time() < deadline:
-                    # every GPU's thread publishing slots, for a full second: its
-                    # broadcast then names the rate it holds, and each rank's
-                    # agent (sampler "auto") refuses a GPU's broadcast that runs
-                    # short from the start
+                    # every GPU's thread publishing slots and holding the rate
+                    # over its last full second: each rank's agent (sampler
+                    # "auto") refuses a GPU's broadcast that runs short, and a
+                    # daemon's first second runs short while its threads start
+                    # (610 samples/s in profiles/round6/g25, which sent every
+                    # rank to in-process sampling).  A daemon publishing but
+                    # still short after 15 s is left to the agents' own check.
                     mon = sidecar.rpc({"fn": "getGpuCounterMonitor"}) or {}
-                    if mon.get("status") == "ok" and all(g.get("slots_published", 0) > 0 and g.get("sample_hz_achieved", 0) > 0
-                                                         for g in mon.get("gpus", [{}])):
-                        break
+                    gpus = mon.get("gpus", [{}]) if mon.get("status") == "ok" else [{}]
+                    if all(g.get("slots_published", 0) > 0 and g.get("sample_hz_achieved", 0) > 0 for g in gpus):
+                        if all(g.get("sample_hz_achieved", 0) >= 0.99 * args.sample_hz for g in gpus):
+                            break
+                        rate_deadline = rate_deadline or time.time() + 15
+                        if time.time() > rate_deadline:
+                            print("bench: the sidecar daemon publishes short of its rate after 15 s: "
+                                  + json.dumps([g.get("sample_hz_achieved") for g in gpus]), file=sys.stderr, flush=True)
+                            break
                     time.sleep(0.2)
                 else:
                     # some GPUs publish: their ranks take the daemon's read, the
